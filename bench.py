@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the batched BallEnv step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--window 10]
+    (N > 1: torchrun --nproc-per-node N ... bench.py --gpus N, one rank per GPU)
+
+A "step" = one be_step launch over the whole local batch: agent move, obstacle
+moves (Philox), collision, reward/done, TimeLimit(1000), in-kernel autoreset and
+the W x W prep_state4 window obs, for every env (ballenv_env.py:232-289 +
+ball_cnn_ac3.py:384-412).  Actions are uniform random indices (the
+random-action rollout of BASELINE configs 2-4), pre-generated in HBM with
+be_sample_actions before the timed region; obstacle draws are Philox.
+Per GPU: --envs envs (default 65536 = config 3, weak scaling across ranks);
+every global env has the same trajectory at any GPU count.
+
+Timed region: the K steps replayed from one HIP graph (captured be_step
+launches; the kernel reads its Philox step counter from device memory, so
+replays advance it), bracketed by barrier + synchronize, max over ranks.
+Kernel duration for the roofline: HIP events around each of K eager launches
+of the same kernel on the same stream, right after the timed region.
+CPU baseline (rank 0, N=1 only, before any GPU work): oracle/py_ballenv.py,
+the reference's algorithm restated in scalar Python, one process per core.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=100)
+    p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    p.add_argument("--window", type=int, default=10)
+    p.add_argument("--mode", choices=["graph", "eager"], default="graph")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-procs", type=int, default=8)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--graph-chunk", type=int, default=250, help="steps per captured graph")
+    return p.parse_args()
+
+
+def cpu_baseline(window, seconds, procs):
+    """Reference algorithm (scalar Python port) on the host cores; no GPU touched."""
+    from oracle import py_ballenv
+    import multiprocessing as mp
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    procs = max(1, min(procs, avail))
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(py_ballenv._worker, [(window, seconds, 1000 + i) for i in range(procs)])
+    steps = sum(s for s, _ in res)
+    el = max(t for _, t in res)
+    return {"value": steps / el, "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} procs x {seconds:.0f} s: single-env BallEnv.step + prep_state4 (W={window}), "
+                      f"13 static + 5 dynamic obstacles, uniform random 9-way actions, reset on done/1000 steps; "
+                      f"{steps} env-steps in {el:.1f} s (oracle/py_ballenv.py, pure Python)"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline(args.window, args.cpu_seconds, args.cpu_procs)
+
+    import torch
+    import torch.distributed as dist
+    import gym_ballenv_amd as gb
+    from gym_ballenv_amd import _abi
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    N, W = args.envs, args.window
+    cfg = gb.EnvConfig()
+    env = gb.BatchedBallEnv(N, W, cfg, device=dev, seed=0xBA11, env_offset=rank * N)
+    B = gb.step_bytes(cfg, W)
+    lib = _abi.lib()
+    K, WU = args.steps, args.warmup
+    actions = env.sample_actions(K + WU, seed=0xBA11)            # (steps, N) u8, resident in HBM
+    env.reset()
+    stream = torch.cuda.current_stream(dev)
+
+    st_ref, out_ref = C.byref(env._st), C.byref(env._out)
+    step_fn, ctx = lib.be_step, env._ctx
+    a0, rowb = actions.data_ptr(), N
+
+    def launch(t, s):
+        rc = step_fn(ctx, st_ref, C.c_void_p(a0 + t * rowb), None, None, out_ref, s)
+        if rc:
+            _abi.check(rc, ctx)
+
+    # warm-up (eager): actions rows K .. K+WU-1
+    s_ptr = C.c_void_p(stream.cuda_stream)
+    for t in range(WU):
+        launch(K + t, s_ptr)
+    torch.cuda.synchronize(dev)
+    env.status()
+
+    graphs = []
+    if args.mode == "graph":
+        cap = torch.cuda.Stream(dev)
+        chunk = max(1, min(args.graph_chunk, K))
+        for c0 in range(0, K, chunk):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                cs = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+                for t in range(c0, min(K, c0 + chunk)):
+                    launch(t, cs)
+            graphs.append(g)
+        # capture does not execute; reset the step counter so timed steps use fresh streams
+        torch.cuda.synchronize(dev)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if args.mode == "graph":
+        for g in graphs:
+            g.replay()
+    else:
+        for t in range(K):
+            launch(t, s_ptr)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed = float(el.item())
+        per_rank = gb.gather_stats(env.stats_buf)            # RCCL all_gather of episode returns
+        ep = gb.combine_stats(per_rank)
+    else:
+        ep = env.episode_stats()
+    env.status()
+
+    # kernel duration: HIP events around each eager launch on the launch stream
+    KD = min(K, 200)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(KD)]
+    for t in range(KD):
+        evs[t][0].record(stream)
+        launch(t, s_ptr)
+        evs[t][1].record(stream)
+    torch.cuda.synchronize(dev)
+    durs = sorted(a.elapsed_time(b) for a, b in evs)           # ms
+    kern_ms = sum(durs) / len(durs)
+    kern_med = durs[len(durs) // 2]
+
+    total_steps = K * N * world
+    value = total_steps / elapsed
+    achieved = B * N / (kern_ms * 1e-3) / 1e9                  # GB/s, algorithmic, per launch
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+    if os.path.exists(pmc):
+        try:
+            d = json.load(open(pmc))
+            if d.get("envs") == N and d.get("window") == W:
+                traffic = d.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        line = {
+            "metric": "env-steps/sec (whole node), batch=65536 envs, window=10; achieved HBM GB/s",
+            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": WU,
+            "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int32+f64", "data": "synthetic",
+            "config": {"workload": f"BallEnv step + prep_state4 window, random actions, {N} envs/GPU, W={W}, "
+                                   "13 static + 5 dynamic obstacles, TimeLimit 1000, autoreset",
+                       "envs_per_gpu": N, "global_envs": N * world, "window": W,
+                       "parallelism": f"env-shard x{world} (no per-step collective)",
+                       "launch": "hipGraph replay of be_step launches" if args.mode == "graph" else "eager"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_per_env_step": B, "kernel_ms_mean": kern_ms, "kernel_ms_median": kern_med,
+                         "kernel": "be_kernel<10, MODE_STEP>"},
+            "cpu_baseline": base,
+            "episodes": ep,
+        }
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,124 @@
+"""ctypes mirror of include/ballenv.h and the loader for libballenv.so.
+
+The shared library is built in-tree (``__graft_entry__.build()`` or
+``python -m gym_ballenv_amd.build``).  There is no fallback: if the library is
+missing or was built for another ABI version, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+ABI_VERSION = 1
+MAX_STATIC, MAX_DYNAMIC, MAX_GOALS, MAX_ACTIONS, MAX_WINDOW = 64, 32, 16, 16, 64
+
+BE_OK, BE_E_INVALID, BE_E_HIP, BE_E_NOMEM, BE_E_DEVICE = 0, -1, -2, -3, -4
+STATUS_BITS = {1: "reset tape exhausted", 2: "reset rejection limit", 4: "action index out of range",
+               8: "dynamic obstacle left the int16 coordinate range",
+               16: "goal change with no other goal (the reference raises ValueError)"}
+
+LIB_NAME = "libballenv.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.realpath(__file__)), LIB_NAME)
+
+# Names declared in include/ballenv.h (checked by tests/test_abi.py).
+EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_bytes", "be_last_error",
+           "be_create", "be_destroy", "be_reset", "be_step", "be_observe", "be_sample_actions",
+           "be_status", "be_get_step_counter", "be_set_step_counter")
+
+
+class BeConfig(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32), ("window", C.c_int32), ("env_offset", C.c_int64), ("seed", C.c_uint64),
+        ("screen_width", C.c_int32), ("screen_height", C.c_int32),
+        ("strip_obs_x", C.c_int32), ("strip_obs_y", C.c_int32),
+        ("strip_goal_x", C.c_int32), ("strip_goal_y", C.c_int32),
+        ("strip_agent_x", C.c_int32), ("strip_agent_y", C.c_int32),
+        ("radius_obstacle", C.c_int32), ("radius_agent", C.c_int32),
+        ("speed_x", C.c_int32), ("speed_y", C.c_int32),
+        ("threshold_goal", C.c_double), ("time_penalty", C.c_double), ("min_spawn_dist", C.c_double),
+        ("num_static", C.c_int32), ("num_dynamic", C.c_int32),
+        ("static_penalty", C.c_double), ("dynamic_penalty", C.c_double),
+        ("goal_change_step", C.c_int32), ("obs_certainty", C.c_int32), ("num_goals", C.c_int32),
+        ("goals", (C.c_int32 * 2) * MAX_GOALS), ("obstacle_speed", C.c_int32 * MAX_DYNAMIC),
+        ("num_actions", C.c_int32), ("actions", (C.c_int32 * 2) * MAX_ACTIONS),
+        ("time_limit", C.c_int32), ("autoreset", C.c_int32),
+    ]
+
+
+class BeState(C.Structure):
+    _fields_ = [("agent", C.c_void_p), ("goal", C.c_void_p), ("prev_dist", C.c_void_p),
+                ("total_dist", C.c_void_p), ("ep_return", C.c_void_p), ("ep_len", C.c_void_p),
+                ("static_obs", C.c_void_p), ("dyn_obs", C.c_void_p), ("dyn_goal", C.c_void_p)]
+
+
+class BeOut(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("obs_f32", C.c_void_p), ("reward", C.c_void_p), ("done", C.c_void_p),
+                ("truncated", C.c_void_p), ("terminal_obs", C.c_void_p), ("final_return", C.c_void_p),
+                ("final_len", C.c_void_p), ("stats", C.c_void_p)]
+
+
+class BallEnvError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libballenv.so (raises if it is absent: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BallEnvError(f"{LIB_PATH} not found: build it with __graft_entry__.build() "
+                           "or `python -m gym_ballenv_amd.build` (no CPU fallback exists)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
+    P = C.POINTER
+    sig = {
+        "be_abi_version": (C.c_int, []),
+        "be_config_default": (C.c_int, [P(BeConfig), i32, i32]),
+        "be_config_check": (C.c_int, [P(BeConfig), C.c_char_p, i32]),
+        "be_step_bytes": (i64, [P(BeConfig)]),
+        "be_last_error": (C.c_char_p, [vp]),
+        "be_create": (C.c_int, [P(BeConfig), i32, P(vp)]),
+        "be_destroy": (C.c_int, [vp]),
+        "be_reset": (C.c_int, [vp, P(BeState), vp, vp, i32, P(BeOut), vp]),
+        "be_step": (C.c_int, [vp, P(BeState), vp, vp, vp, P(BeOut), vp]),
+        "be_observe": (C.c_int, [vp, P(BeState), P(BeOut), vp]),
+        "be_sample_actions": (C.c_int, [vp, vp, i32, u64, vp]),
+        "be_status": (C.c_int, [vp, P(i32), vp]),
+        "be_get_step_counter": (C.c_int, [vp, P(u64), vp]),
+        "be_set_step_counter": (C.c_int, [vp, u64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    v = L.be_abi_version()
+    if v != ABI_VERSION:
+        raise BallEnvError(f"{LIB_PATH} has ABI {v}, expected {ABI_VERSION}: rebuild it")
+    _lib = L
+    return L
+
+
+def check(rc: int, ctx=None) -> None:
+    if rc != BE_OK:
+        msg = lib().be_last_error(ctx)
+        raise BallEnvError(f"libballenv error {rc}: {msg.decode() if msg else ''}")
+
+
+def default_config(num_envs: int, window: int) -> BeConfig:
+    c = BeConfig()
+    check(lib().be_config_default(C.byref(c), num_envs, window))
+    return c
+
+
+def config_check(c: BeConfig) -> str:
+    """'' if valid, else the library's message (pure host code, no GPU needed)."""
+    buf = C.create_string_buffer(256)
+    rc = lib().be_config_check(C.byref(c), buf, 256)
+    return "" if rc == BE_OK else buf.value.decode()
+
+
+def step_bytes(c: BeConfig) -> int:
+    return int(lib().be_step_bytes(C.byref(c)))

@@ -1,0 +1,257 @@
+"""BatchedBallEnv: N independent BallEnvs as a struct-of-arrays on one GPU.
+
+Host side of the drop-in boundary.  The per-env state lives in caller-owned
+PyTorch tensors (env index = unit stride); every reset/step/observe is one
+asynchronous launch of the HIP kernels in libballenv.so on the current torch
+stream, through the C ABI of include/ballenv.h.  Nothing here computes physics
+or observations on the CPU, and there is no fallback path.
+
+Reference surface this mirrors (gym.Env protocol used by examples/ball_cnn_ac3.py):
+* ``reset()``  <- BallEnv.reset        gym_ballenv/envs/ballenv_env.py:113-167 (+ prep_state4)
+* ``step(a)``  <- BallEnv.step         ballenv_env.py:232-289, then prep_state4
+                  (examples/ball_cnn_ac3.py:384-412), under the TimeLimit(1000) of
+                  gym_ballenv/__init__.py:4-11
+* ``customize_environment(args)``      ballenv_env.py:87-109
+* ``total_reward_accumulated``         ballenv_env.py:66,129,280 (here an (N,) f64 view)
+* ``observation_space/action_space``   the shapes step() really returns / accepts
+                  (the reference declares Box(2)/Discrete(4), ballenv_env.py:57-58, Q11)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Optional
+
+import torch
+
+from . import _abi
+from .config import EnvConfig
+from .spaces import Box, Discrete
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+class BatchedBallEnv:
+    """``num_envs`` BallEnvs stepped by one kernel launch per call.
+
+    Returned tensors (obs, reward, done, info entries) are views of internal
+    buffers that the next call overwrites; ``.clone()`` what you keep.
+    """
+
+    def __init__(self, num_envs: int, window: int = 10, config: Optional[EnvConfig] = None,
+                 device="cuda", seed: int = 0xBA11, env_offset: int = 0, obs_f32: bool = False,
+                 track_stats: bool = True, terminal_obs: bool = False):
+        self.num_envs, self.window = int(num_envs), int(window)
+        self.cfg = config if config is not None else EnvConfig()
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("BatchedBallEnv runs on a GPU device only (no CPU fallback)")
+        self.seed, self.env_offset = int(seed), int(env_offset)
+        self.obs_dim = 4 + self.window * self.window
+        self._want_f32, self._want_terminal, self._track_stats = obs_f32, terminal_obs, track_stats
+        self._lib = _abi.lib()
+        self._ctx = None
+        self._alloc()
+        self._create_ctx()
+
+    # ------------------------------------------------------------------ setup
+    def _alloc(self):
+        N, dev, cfg = self.num_envs, self.device, self.cfg
+        z = lambda *shape, dt: torch.zeros(*shape, dtype=dt, device=dev)  # noqa: E731
+        self.agent = z(N, 2, dt=torch.int16)
+        self.goal = z(N, 2, dt=torch.int16)
+        self.prev_dist = z(N, dt=torch.float64)
+        self.total_dist = z(N, dt=torch.float64)
+        self.ep_return = z(N, dt=torch.float64)
+        self.ep_len = z(N, dt=torch.int32)
+        self.static_obs = z(max(cfg.num_static, 1), N, 2, dt=torch.int16)
+        self.dyn_obs = z(max(cfg.num_dynamic, 1), N, 2, dt=torch.int16)
+        self.dyn_goal = z(max(cfg.num_dynamic, 1), N, dt=torch.uint8)
+        F = self.obs_dim
+        self.obs = z(N, F, dt=torch.uint8)
+        self.obs_f32 = z(N, F, dt=torch.float32) if self._want_f32 else None
+        self.reward = z(N, dt=torch.float64)
+        self.done = z(N, dt=torch.bool)
+        self.truncated = z(N, dt=torch.bool)
+        self.final_return = z(N, dt=torch.float64)
+        self.final_len = z(N, dt=torch.int32)
+        self.terminal_obs = z(N, F, dt=torch.uint8) if self._want_terminal else None
+        self.stats_buf = z(8, dt=torch.float64)
+        self.clear_stats()
+        self._st = _abi.BeState(*[t.data_ptr() for t in (self.agent, self.goal, self.prev_dist, self.total_dist,
+                                                        self.ep_return, self.ep_len, self.static_obs,
+                                                        self.dyn_obs, self.dyn_goal)])
+        self._out = _abi.BeOut(self.obs.data_ptr(), _ptr(self.obs_f32), self.reward.data_ptr(),
+                               self.done.data_ptr(), self.truncated.data_ptr(), _ptr(self.terminal_obs),
+                               self.final_return.data_ptr(), self.final_len.data_ptr(),
+                               self.stats_buf.data_ptr() if self._track_stats else None)
+
+    def _create_ctx(self):
+        if self._ctx is not None:
+            self._lib.be_destroy(self._ctx)
+            self._ctx = None
+        self._abi_cfg = self.cfg.to_abi(self.num_envs, self.window, self.env_offset, self.seed)
+        msg = _abi.config_check(self._abi_cfg)
+        if msg:
+            raise ValueError(f"invalid BallEnv config: {msg}")
+        ctx = C.c_void_p()
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        _abi.check(self._lib.be_create(C.byref(self._abi_cfg), dev, C.byref(ctx)))
+        self._ctx = ctx
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ gym surface
+    @property
+    def observation_space(self) -> Box:
+        return Box(0.0, 1.0, (self.obs_dim,))
+
+    @property
+    def action_space(self) -> Discrete:
+        return Discrete(len(self.cfg.actions))
+
+    @property
+    def total_reward_accumulated(self) -> torch.Tensor:
+        return self.ep_return
+
+    def customize_environment(self, args) -> None:
+        """ballenv_env.py:87-109: reconfigure from ball_cnn_ac3.py-style argparse args."""
+        self.cfg = EnvConfig.from_args(args, self.cfg)
+        self._alloc()
+        self._create_ctx()
+
+    def reset(self, mask: Optional[torch.Tensor] = None, reset_tape: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Reset all envs (or those with mask != 0); returns the obs of every env.
+
+        ``reset_tape``: optional (L, N) int16 randint values in the reference's
+        call order (parity mode); otherwise Philox draws keyed by global env id.
+        """
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            self._check_shape(m, (self.num_envs,), "mask")
+        L = 0
+        if reset_tape is not None:
+            reset_tape = reset_tape.to(device=self.device, dtype=torch.int16).contiguous()
+            if reset_tape.dim() != 2 or reset_tape.shape[1] != self.num_envs:
+                raise ValueError("reset_tape must be (L, num_envs) int16")
+            L = reset_tape.shape[0]
+        _abi.check(self._lib.be_reset(self._ctx, C.byref(self._st), _ptr(m), _ptr(reset_tape), L,
+                                      C.byref(self._out), self._stream()), self._ctx)
+        self._keep = (m, reset_tape)
+        return self.obs_f32 if self._want_f32 else self.obs
+
+    def step(self, actions: Optional[torch.Tensor] = None, deltas: Optional[torch.Tensor] = None,
+             draw_tape: Optional[torch.Tensor] = None):
+        """One step of every env.
+
+        actions: (N,) integer indices into ``cfg.actions`` (the move_list of
+        ball_cnn_ac3.py:530); or deltas: (N, 2) raw (dx, dy) as BallEnv.step takes;
+        neither: uniformly sampled actions (Philox, keyed by global env id).
+        draw_tape: (Nd, 2, N) int16 obstacle-move randint values (parity mode).
+        Returns (obs, reward f64, done bool, info).
+        """
+        a = d = t = None
+        if actions is not None:
+            a = actions if actions.dtype == torch.uint8 else actions.to(torch.uint8)
+            if a.device != self.device:
+                a = a.to(self.device)
+            a = a.contiguous()
+            self._check_shape(a, (self.num_envs,), "actions")
+        elif deltas is not None:
+            d = deltas.to(device=self.device, dtype=torch.int16).contiguous()
+            self._check_shape(d, (self.num_envs, 2), "deltas")
+        if draw_tape is not None:
+            t = draw_tape.to(device=self.device, dtype=torch.int16).contiguous()
+            if self.cfg.num_dynamic:
+                self._check_shape(t, (self.cfg.num_dynamic, 2, self.num_envs), "draw_tape")
+        _abi.check(self._lib.be_step(self._ctx, C.byref(self._st), _ptr(a), _ptr(d), _ptr(t),
+                                     C.byref(self._out), self._stream()), self._ctx)
+        self._keep = (a, d, t)
+        info = {"truncated": self.truncated, "final_return": self.final_return, "final_len": self.final_len}
+        if self.terminal_obs is not None:
+            info["terminal_obs"] = self.terminal_obs
+        return (self.obs_f32 if self._want_f32 else self.obs), self.reward, self.done, info
+
+    def observe(self) -> torch.Tensor:
+        """prep_state4 of the current state (no state change)."""
+        _abi.check(self._lib.be_observe(self._ctx, C.byref(self._st), C.byref(self._out), self._stream()), self._ctx)
+        return self.obs_f32 if self._want_f32 else self.obs
+
+    def sample_actions(self, steps: int, seed: int = 0xBA11) -> torch.Tensor:
+        """(steps, N) u8 uniform action indices from Philox(seed; global env id, t)."""
+        out = torch.empty(steps, self.num_envs, dtype=torch.uint8, device=self.device)
+        _abi.check(self._lib.be_sample_actions(self._ctx, out.data_ptr(), int(steps), int(seed) & (2**64 - 1),
+                                               self._stream()), self._ctx)
+        return out
+
+    # ------------------------------------------------------------------ bookkeeping
+    def status(self) -> int:
+        """Synchronise and read (then clear) the device status word; raises on error bits."""
+        v = C.c_int32()
+        _abi.check(self._lib.be_status(self._ctx, C.byref(v), self._stream()), self._ctx)
+        if v.value:
+            bits = [txt for bit, txt in _abi.STATUS_BITS.items() if v.value & bit]
+            raise _abi.BallEnvError("device status: " + "; ".join(bits))
+        return 0
+
+    @property
+    def step_counter(self) -> int:
+        v = C.c_uint64()
+        _abi.check(self._lib.be_get_step_counter(self._ctx, C.byref(v), self._stream()), self._ctx)
+        return int(v.value)
+
+    @step_counter.setter
+    def step_counter(self, value: int) -> None:
+        _abi.check(self._lib.be_set_step_counter(self._ctx, int(value), self._stream()), self._ctx)
+
+    def clear_stats(self) -> None:
+        self.stats_buf.zero_()
+        self.stats_buf[4] = math.inf
+        self.stats_buf[5] = -math.inf
+
+    def episode_stats(self) -> dict:
+        s = self.stats_buf.cpu().tolist()
+        n = s[0]
+        return {"episodes": int(n), "mean_return": s[1] / n if n else float("nan"),
+                "sum_return": s[1], "sum_return_sq": s[2], "mean_length": s[3] / n if n else float("nan"),
+                "min_return": s[4], "max_return": s[5]}
+
+    STATE_KEYS = ("agent", "goal", "prev_dist", "total_dist", "ep_return", "ep_len", "static_obs", "dyn_obs",
+                  "dyn_goal")
+
+    def state_dict(self) -> dict:
+        """SoA snapshot (env-state checkpoint; SURVEY §5 'Checkpoint / resume')."""
+        d = {k: getattr(self, k).clone() for k in self.STATE_KEYS}
+        d["step_counter"] = torch.tensor(self.step_counter, dtype=torch.int64)
+        return d
+
+    def load_state_dict(self, d: dict) -> None:
+        for k in self.STATE_KEYS:
+            src = d[k]
+            dst = getattr(self, k)
+            if tuple(src.shape) != tuple(dst.shape):
+                raise ValueError(f"state '{k}': shape {tuple(src.shape)} != {tuple(dst.shape)}")
+            dst.copy_(src.to(device=self.device, dtype=dst.dtype))
+        if "step_counter" in d:
+            self.step_counter = int(d["step_counter"])
+
+    def close(self) -> None:
+        if self._ctx is not None:
+            torch.cuda.synchronize(self.device)
+            self._lib.be_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _check_shape(t: torch.Tensor, shape, name: str) -> None:
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")

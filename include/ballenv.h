@@ -1,0 +1,183 @@
+/*
+ * ballenv.h -- C ABI of the MI355X batched BallEnv step engine (libballenv.so).
+ *
+ * The reference (ranok92/gym-ballenv) is pure Python; the "FFI" this library
+ * stands behind is the gym.Env protocol that examples/ball_cnn_ac3.py drives:
+ *
+ *   be_config            <- BallEnv.__init__ constants + customize_environment(args)
+ *                           (gym_ballenv/envs/ballenv_env.py:11-18, 43-85, 87-109;
+ *                            argparse defaults examples/ball_cnn_ac3.py:37-59)
+ *   be_reset             <- BallEnv.reset()            (ballenv_env.py:113-167)
+ *   be_step              <- BallEnv.step(action)       (ballenv_env.py:232-289, incl.
+ *                           move_obstacles :323-353, calculate_reward :200-229,
+ *                           check_overlap :185-191) followed by
+ *                           prep_state4(state, W)      (examples/ball_cnn_ac3.py:384-412,
+ *                           quadrant prep_state2 :330-352) and the gym TimeLimit
+ *                           registered with timestep_limit=1000 (gym_ballenv/__init__.py:4-11)
+ *   be_observe           <- prep_state4(state, W) on the current state
+ *
+ * Conventions
+ *   - Plain C: no C++ types, no exceptions cross this boundary.  Every entry
+ *     point returns BE_OK (0) or a negative BE_E* code; be_last_error() gives
+ *     the message for the last failing call on that context (or, for a NULL
+ *     context, the last process-wide failure).
+ *   - All per-env device buffers are allocated and owned by the CALLER
+ *     (PyTorch tensors); the library owns only a few words of device scratch
+ *     (step counter, status word).  Every compute call is asynchronous and
+ *     ordered on the hipStream_t the caller passes (as void*).
+ *   - Layout is struct-of-arrays with the env index as the unit-stride axis:
+ *     an (x, y) position is two int16 in one 32-bit word (x low, y high),
+ *     i.e. an (N, 2) int16 array; per-obstacle arrays are (K, N, 2) int16.
+ *   - One context per (device, config).  No internal threads.
+ */
+#ifndef BALLENV_H
+#define BALLENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BE_ABI_VERSION 1
+
+#define BE_MAX_STATIC   64
+#define BE_MAX_DYNAMIC  32
+#define BE_MAX_GOALS    16
+#define BE_MAX_ACTIONS  16
+#define BE_MAX_WINDOW   64
+
+enum {
+  BE_OK = 0,
+  BE_E_INVALID = -1,   /* bad argument / config */
+  BE_E_HIP = -2,       /* HIP runtime error */
+  BE_E_NOMEM = -3,
+  BE_E_DEVICE = -4     /* device-side status word reported a failure */
+};
+
+/* Device-side status bits (be_status). */
+enum {
+  BE_STATUS_RESET_TAPE_EXHAUSTED = 1,  /* a reset consumed more draws than its tape held */
+  BE_STATUS_REJECTION_LIMIT = 2,       /* a reset rejection loop hit its bound */
+  BE_STATUS_BAD_ACTION = 4,            /* action index >= num_actions */
+  BE_STATUS_COORD_RANGE = 8,           /* a dynamic obstacle left the int16 range */
+  BE_STATUS_NO_GOAL = 16               /* goal change with no other goal (reference raises) */
+};
+
+typedef struct be_config {
+  int32_t num_envs;          /* N on this device */
+  int32_t window;            /* W of prep_state4 (1..BE_MAX_WINDOW) */
+  int64_t env_offset;        /* global id of local env 0 (rank * N); keys the Philox streams */
+  uint64_t seed;             /* Philox key for resets / obstacle moves / sampled actions */
+
+  /* field and spawn strips, ballenv_env.py:11-18 */
+  int32_t screen_width, screen_height;                 /* 500, 500 */
+  int32_t strip_obs_x, strip_obs_y;                    /* 0, 20 */
+  int32_t strip_goal_x, strip_goal_y;                  /* 500, 20 */
+  int32_t strip_agent_x, strip_agent_y;                /* 500, 10 */
+
+  /* BallEnv.__init__ constants, ballenv_env.py:49-65 */
+  int32_t radius_obstacle;   /* radius_rand_person = 20 */
+  int32_t radius_agent;      /* radius_ctrl_person = 5 */
+  int32_t speed_x, speed_y;  /* speedx/y_ctrl_person = 1 (also the window cell step) */
+  double threshold_goal;     /* 10 (strict <) */
+  double time_penalty;       /* timepenalty = 0 */
+  double min_spawn_dist;     /* reset re-sample distance, ballenv_env.py:122 (50) */
+
+  /* customize_environment(args), ballenv_env.py:87-109 */
+  int32_t num_static;        /* args.static_obstacles (13) */
+  int32_t num_dynamic;       /* args.dynamic_obstacles (5) */
+  double static_penalty;     /* args.static_penalty[1]  (threshold_2_penalty, 1) */
+  double dynamic_penalty;    /* args.dynamic_penalty[1] (8000) */
+  int32_t goal_change_step;  /* args.time_step_for_change (50) */
+  int32_t obs_certainty;     /* args.rd_th_obs (60): P(directed move) in percent */
+  int32_t num_goals;         /* len(args.obs_goal_position) */
+  int32_t goals[BE_MAX_GOALS][2];
+  int32_t obstacle_speed[BE_MAX_DYNAMIC];
+
+  /* action table: index -> (dx, dy); default = move_list of ball_cnn_ac3.py:530 */
+  int32_t num_actions;
+  int32_t actions[BE_MAX_ACTIONS][2];
+
+  int32_t time_limit;        /* gym TimeLimit max_episode_steps (1000); 0 = none */
+  int32_t autoreset;         /* 1: a done env is reset inside be_step (vector-env semantics) */
+} be_config;
+
+/* Per-env state, all device pointers owned by the caller. */
+typedef struct be_state {
+  int32_t* agent;       /* (N)  int16x2 packed (x, y)            state[0]          */
+  int32_t* goal;        /* (N)  int16x2 packed                    state[1]          */
+  double* prev_dist;    /* (N)  f64                               state[2] / old_dist */
+  double* total_dist;   /* (N)  f64                               total_distance    */
+  double* ep_return;    /* (N)  f64                               total_reward_accumulated */
+  int32_t* ep_len;      /* (N)  steps since reset (TimeLimit elapsed; also the obstacles' curr_counter phase) */
+  int32_t* static_obs;  /* (Ns, N) int16x2 packed                 static_obstacle_list */
+  int32_t* dyn_obs;     /* (Nd, N) int16x2 packed                 dynamic_obstacle_list */
+  uint8_t* dyn_goal;    /* (Nd, N) index into goals               obstacle.curr_goal */
+} be_state;
+
+/* Step / observe outputs (device pointers; NULL = not requested). */
+typedef struct be_out {
+  uint8_t* obs;           /* (N, 4+W*W) u8 0/1: quadrant one-hot ++ W*W window */
+  float* obs_f32;         /* (N, 4+W*W) f32 copy of the same (what prep_state4 returns) */
+  double* reward;         /* (N) f64 (be_step only) */
+  uint8_t* done;          /* (N) 0/1 (be_step only) */
+  uint8_t* truncated;     /* (N) 0/1: done came from the time limit alone */
+  uint8_t* terminal_obs;  /* (N, 4+W*W): obs of the terminal state, rows of done envs only (autoreset) */
+  double* final_return;   /* (N): episode return, written for done envs only */
+  int32_t* final_len;     /* (N): episode length, written for done envs only */
+  double* stats;          /* (8) f64 accumulators: [0]=episodes, [1]=sum return, [2]=sum return^2,
+                             [3]=sum length, [4]=min return, [5]=max return; caller initialises
+                             [4]=+inf [5]=-inf, the rest 0 */
+} be_out;
+
+typedef struct be_ctx be_ctx;
+
+/* ---- pure host functions (no GPU needed) ---- */
+int be_abi_version(void);
+/* Fill cfg with the ball_cnn_ac3.py / BallEnv defaults for N envs and window W. */
+int be_config_default(be_config* cfg, int32_t num_envs, int32_t window);
+/* Validate cfg; on failure returns BE_E_INVALID and writes a message into msg. */
+int be_config_check(const be_config* cfg, char* msg, int32_t msg_len);
+/* Bytes of HBM traffic per env-step the step kernel is designed to move (u8 obs). */
+int64_t be_step_bytes(const be_config* cfg);
+const char* be_last_error(const be_ctx* ctx);
+
+/* ---- device functions ---- */
+int be_create(const be_config* cfg, int32_t device, be_ctx** out);
+int be_destroy(be_ctx* ctx);
+
+/* Reset envs (all, or those with mask[i] != 0) and write the obs of every env.
+ * reset_tape == NULL: draws come from Philox(seed; global env id, reset epoch).
+ * reset_tape != NULL: (tape_len, N) int16, the randint values the reference's
+ * reset() would consume, in call order (parity mode).                           */
+int be_reset(be_ctx* ctx, const be_state* st, const uint8_t* mask,
+             const int16_t* reset_tape, int32_t tape_len, const be_out* out, void* stream);
+
+/* One step of every env.
+ * actions:       (N) u8 index into cfg.actions, or NULL to use action_deltas.
+ * action_deltas: (N, 2) int16 raw (dx, dy) as BallEnv.step accepts, or NULL
+ *                (both NULL: actions are sampled uniformly from Philox).
+ * draw_tape:     (Nd, 2, N) int16: the move_obstacles randint values of this
+ *                step per obstacle in call order (parity mode), or NULL (Philox). */
+int be_step(be_ctx* ctx, const be_state* st, const uint8_t* actions, const int16_t* action_deltas,
+            const int16_t* draw_tape, const be_out* out, void* stream);
+
+/* prep_state4 of the current state of every env (no state change). */
+int be_observe(be_ctx* ctx, const be_state* st, const be_out* out, void* stream);
+
+/* Fill actions_out (steps, N) u8 with uniform action indices from Philox keyed
+ * by (seed, global env id): identical per global env at any GPU count.         */
+int be_sample_actions(be_ctx* ctx, uint8_t* actions_out, int32_t steps, uint64_t seed, void* stream);
+
+/* Synchronise the context's stream work and read (then clear) the device status word. */
+int be_status(be_ctx* ctx, int32_t* status_out, void* stream);
+
+/* Number of be_step calls issued (device step counter keys the Philox stream). */
+int be_get_step_counter(be_ctx* ctx, uint64_t* value, void* stream);
+int be_set_step_counter(be_ctx* ctx, uint64_t value, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BALLENV_H */

@@ -1,0 +1,113 @@
+"""ctypes binding of oracle/liboracle.so (the C restatement) on numpy SoA dicts.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  The SoA dict uses the same
+keys, dtypes and layouts as BatchedBallEnv's tensors:
+agent/goal (N,2) int16, prev_dist/total_dist/ep_return (N,) f64, ep_len (N,)
+int32, static_obs (Ns,N,2) int16, dyn_obs (Nd,N,2) int16, dyn_goal (Nd,N) u8.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.realpath(__file__))
+SO = os.path.join(HERE, "liboracle.so")
+STATE_KEYS = ("agent", "goal", "prev_dist", "total_dist", "ep_return", "ep_len", "static_obs", "dyn_obs", "dyn_goal")
+
+
+def build(force: bool = False) -> str:
+    src = [os.path.join(HERE, "ballenv_oracle.c"), os.path.join(HERE, "..", "include", "ballenv.h")]
+    if force or not os.path.exists(SO) or any(os.path.getmtime(s) > os.path.getmtime(SO) for s in src):
+        subprocess.run(["make", "-C", HERE, "-B" if force else "liboracle.so"], check=True,
+                       stdout=subprocess.DEVNULL)
+    return SO
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(SO)
+        vp, i32, u64 = C.c_void_p, C.c_int32, C.c_uint64
+        L.orc_step.argtypes = [vp, vp, vp, vp, vp, vp, u64, vp]
+        L.orc_reset.argtypes = [vp, vp, vp, vp, i32, vp, u64, vp]
+        L.orc_observe.argtypes = [vp, vp, vp]
+        L.orc_sample_actions.argtypes = [vp, vp, i32, u64]
+        L.orc_philox4x32_10.argtypes = [vp, C.c_uint32, C.c_uint32, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def new_state(cfg, n=None):
+    n = cfg.num_envs if n is None else n
+    ns, nd = max(cfg.num_static, 1), max(cfg.num_dynamic, 1)
+    return dict(agent=np.zeros((n, 2), np.int16), goal=np.zeros((n, 2), np.int16),
+                prev_dist=np.zeros(n), total_dist=np.zeros(n), ep_return=np.zeros(n),
+                ep_len=np.zeros(n, np.int32), static_obs=np.zeros((ns, n, 2), np.int16),
+                dyn_obs=np.zeros((nd, n, 2), np.int16), dyn_goal=np.zeros((nd, n), np.uint8))
+
+
+def _state_struct(st):
+    from gym_ballenv_amd._abi import BeState
+    for k in STATE_KEYS:
+        assert st[k].flags.c_contiguous, k
+    return BeState(*[_p(st[k]) for k in STATE_KEYS])
+
+
+def new_out(cfg, f32=False, terminal=False):
+    n, F = cfg.num_envs, 4 + cfg.window * cfg.window
+    o = dict(obs=np.zeros((n, F), np.uint8), reward=np.zeros(n), done=np.zeros(n, np.uint8),
+             truncated=np.zeros(n, np.uint8), final_return=np.zeros(n), final_len=np.zeros(n, np.int32),
+             stats=np.array([0, 0, 0, 0, np.inf, -np.inf, 0, 0], np.float64))
+    o["obs_f32"] = np.zeros((n, F), np.float32) if f32 else None
+    o["terminal_obs"] = np.zeros((n, F), np.uint8) if terminal else None
+    return o
+
+
+def _out_struct(o):
+    from gym_ballenv_amd._abi import BeOut
+    return BeOut(_p(o["obs"]), _p(o.get("obs_f32")), _p(o.get("reward")), _p(o.get("done")),
+                 _p(o.get("truncated")), _p(o.get("terminal_obs")), _p(o.get("final_return")),
+                 _p(o.get("final_len")), _p(o.get("stats")))
+
+
+def step(cfg, st, out, actions=None, deltas=None, tape=None, step_counter=0):
+    status = C.c_int32(0)
+    lib().orc_step(C.byref(cfg), C.byref(_state_struct(st)), _p(actions), _p(deltas), _p(tape),
+                   C.byref(_out_struct(out)), int(step_counter), C.byref(status))
+    return status.value
+
+
+def reset(cfg, st, out, mask=None, tape=None, step_counter=0):
+    status = C.c_int32(0)
+    L = 0 if tape is None else tape.shape[0]
+    lib().orc_reset(C.byref(cfg), C.byref(_state_struct(st)), _p(mask), _p(tape), L,
+                    C.byref(_out_struct(out)) if out is not None else None, int(step_counter), C.byref(status))
+    return status.value
+
+
+def observe(cfg, st, out):
+    lib().orc_observe(C.byref(cfg), C.byref(_state_struct(st)), C.byref(_out_struct(out)))
+
+
+def sample_actions(cfg, steps, seed):
+    a = np.zeros((steps, cfg.num_envs), np.uint8)
+    lib().orc_sample_actions(C.byref(cfg), _p(a), int(steps), int(seed))
+    return a
+
+
+def philox(ctr, key):
+    c = np.array(ctr, np.uint32)
+    o = np.zeros(4, np.uint32)
+    lib().orc_philox4x32_10(_p(c), int(key[0]), int(key[1]), _p(o))
+    return [int(v) for v in o]
