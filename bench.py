@@ -13,9 +13,10 @@ be_sample_actions before the timed region; obstacle draws are Philox.
 Per GPU: --envs envs (default 65536 = config 3, weak scaling across ranks);
 every global env has the same trajectory at any GPU count.
 
-Timed region: the K steps replayed from one HIP graph (captured be_step
-launches; the kernel reads its Philox step counter from device memory, so
-replays advance it), bracketed by barrier + synchronize, max over ranks.
+Timed region: the K steps replayed from HIP graphs of captured be_step
+launches (Philox draws are keyed by per-env state -- env id, episode,
+ep_len -- so replays are fresh steps), bracketed by barrier + synchronize,
+max over ranks.
 Kernel duration for the roofline: HIP events around each of K eager launches
 of the same kernel on the same stream, right after the timed region.
 CPU baseline (rank 0, N=1 only, before any GPU work): oracle/py_ballenv.py,
@@ -128,7 +129,6 @@ def main():
                 for t in range(c0, min(K, c0 + chunk)):
                     launch(t, cs)
             graphs.append(g)
-        # capture does not execute; reset the step counter so timed steps use fresh streams
         torch.cuda.synchronize(dev)
 
     if world > 1:

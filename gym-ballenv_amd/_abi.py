@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_STATIC, MAX_DYNAMIC, MAX_GOALS, MAX_ACTIONS, MAX_WINDOW = 64, 32, 16, 16, 64
 
 BE_OK, BE_E_INVALID, BE_E_HIP, BE_E_NOMEM, BE_E_DEVICE = 0, -1, -2, -3, -4
@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.realpath(__file__)), LIB_NAME)
 # Names declared in include/ballenv.h (checked by tests/test_abi.py).
 EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_bytes", "be_last_error",
            "be_create", "be_destroy", "be_reset", "be_step", "be_observe", "be_sample_actions",
-           "be_status", "be_get_step_counter", "be_set_step_counter")
+           "be_status")
 
 
 class BeConfig(C.Structure):
@@ -47,7 +47,7 @@ class BeConfig(C.Structure):
 
 class BeState(C.Structure):
     _fields_ = [("agent", C.c_void_p), ("goal", C.c_void_p), ("prev_dist", C.c_void_p),
-                ("total_dist", C.c_void_p), ("ep_return", C.c_void_p), ("ep_len", C.c_void_p),
+                ("total_dist", C.c_void_p), ("ep_return", C.c_void_p), ("ep_len", C.c_void_p), ("episode", C.c_void_p),
                 ("static_obs", C.c_void_p), ("dyn_obs", C.c_void_p), ("dyn_goal", C.c_void_p)]
 
 
@@ -88,8 +88,6 @@ def lib() -> C.CDLL:
         "be_observe": (C.c_int, [vp, P(BeState), P(BeOut), vp]),
         "be_sample_actions": (C.c_int, [vp, vp, i32, u64, vp]),
         "be_status": (C.c_int, [vp, P(i32), vp]),
-        "be_get_step_counter": (C.c_int, [vp, P(u64), vp]),
-        "be_set_step_counter": (C.c_int, [vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -40,6 +40,10 @@ class BatchedBallEnv:
     buffers that the next call overwrites; ``.clone()`` what you keep.
     """
 
+    # SoA state tensors, in be_state field order (include/ballenv.h)
+    STATE_KEYS = ("agent", "goal", "prev_dist", "total_dist", "ep_return", "ep_len", "episode", "static_obs",
+                  "dyn_obs", "dyn_goal")
+
     def __init__(self, num_envs: int, window: int = 10, config: Optional[EnvConfig] = None,
                  device="cuda", seed: int = 0xBA11, env_offset: int = 0, obs_f32: bool = False,
                  track_stats: bool = True, terminal_obs: bool = False):
@@ -66,6 +70,7 @@ class BatchedBallEnv:
         self.total_dist = z(N, dt=torch.float64)
         self.ep_return = z(N, dt=torch.float64)
         self.ep_len = z(N, dt=torch.int32)
+        self.episode = z(N, dt=torch.int32)      # uint32 on the device side
         self.static_obs = z(max(cfg.num_static, 1), N, 2, dt=torch.int16)
         self.dyn_obs = z(max(cfg.num_dynamic, 1), N, 2, dt=torch.int16)
         self.dyn_goal = z(max(cfg.num_dynamic, 1), N, dt=torch.uint8)
@@ -80,9 +85,7 @@ class BatchedBallEnv:
         self.terminal_obs = z(N, F, dt=torch.uint8) if self._want_terminal else None
         self.stats_buf = z(8, dt=torch.float64)
         self.clear_stats()
-        self._st = _abi.BeState(*[t.data_ptr() for t in (self.agent, self.goal, self.prev_dist, self.total_dist,
-                                                        self.ep_return, self.ep_len, self.static_obs,
-                                                        self.dyn_obs, self.dyn_goal)])
+        self._st = _abi.BeState(*[getattr(self, k).data_ptr() for k in self.STATE_KEYS])
         self._out = _abi.BeOut(self.obs.data_ptr(), _ptr(self.obs_f32), self.reward.data_ptr(),
                                self.done.data_ptr(), self.truncated.data_ptr(), _ptr(self.terminal_obs),
                                self.final_return.data_ptr(), self.final_len.data_ptr(),
@@ -198,16 +201,6 @@ class BatchedBallEnv:
             raise _abi.BallEnvError("device status: " + "; ".join(bits))
         return 0
 
-    @property
-    def step_counter(self) -> int:
-        v = C.c_uint64()
-        _abi.check(self._lib.be_get_step_counter(self._ctx, C.byref(v), self._stream()), self._ctx)
-        return int(v.value)
-
-    @step_counter.setter
-    def step_counter(self, value: int) -> None:
-        _abi.check(self._lib.be_set_step_counter(self._ctx, int(value), self._stream()), self._ctx)
-
     def clear_stats(self) -> None:
         self.stats_buf.zero_()
         self.stats_buf[4] = math.inf
@@ -220,14 +213,10 @@ class BatchedBallEnv:
                 "sum_return": s[1], "sum_return_sq": s[2], "mean_length": s[3] / n if n else float("nan"),
                 "min_return": s[4], "max_return": s[5]}
 
-    STATE_KEYS = ("agent", "goal", "prev_dist", "total_dist", "ep_return", "ep_len", "static_obs", "dyn_obs",
-                  "dyn_goal")
 
     def state_dict(self) -> dict:
         """SoA snapshot (env-state checkpoint; SURVEY §5 'Checkpoint / resume')."""
-        d = {k: getattr(self, k).clone() for k in self.STATE_KEYS}
-        d["step_counter"] = torch.tensor(self.step_counter, dtype=torch.int64)
-        return d
+        return {k: getattr(self, k).clone() for k in self.STATE_KEYS}
 
     def load_state_dict(self, d: dict) -> None:
         for k in self.STATE_KEYS:
@@ -235,9 +224,9 @@ class BatchedBallEnv:
             dst = getattr(self, k)
             if tuple(src.shape) != tuple(dst.shape):
                 raise ValueError(f"state '{k}': shape {tuple(src.shape)} != {tuple(dst.shape)}")
+            if hasattr(torch, "uint32") and src.dtype == torch.uint32:
+                src = src.view(torch.int32)
             dst.copy_(src.to(device=self.device, dtype=dst.dtype))
-        if "step_counter" in d:
-            self.step_counter = int(d["step_counter"])
 
     def close(self) -> None:
         if self._ctx is not None:

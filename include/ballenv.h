@@ -22,13 +22,17 @@
  *     the message for the last failing call on that context (or, for a NULL
  *     context, the last process-wide failure).
  *   - All per-env device buffers are allocated and owned by the CALLER
- *     (PyTorch tensors); the library owns only a few words of device scratch
- *     (step counter, status word).  Every compute call is asynchronous and
+ *     (PyTorch tensors); the library owns one word of device scratch (the
+ *     status word).  Every compute call is asynchronous and
  *     ordered on the hipStream_t the caller passes (as void*).
  *   - Layout is struct-of-arrays with the env index as the unit-stride axis:
  *     an (x, y) position is two int16 in one 32-bit word (x low, y high),
  *     i.e. an (N, 2) int16 array; per-obstacle arrays are (K, N, 2) int16.
  *   - One context per (device, config).  No internal threads.
+ *   - Randomness (perf mode): Philox4x32-10 keyed by cfg.seed with counter
+ *     (global env id, episode, ep_len, purpose|sub).  Every draw is a pure
+ *     function of per-env state, so results do not depend on launch order,
+ *     graph replay, or how the batch is split across GPUs.
  */
 #ifndef BALLENV_H
 #define BALLENV_H
@@ -39,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BE_ABI_VERSION 1
+#define BE_ABI_VERSION 2
 
 #define BE_MAX_STATIC   64
 #define BE_MAX_DYNAMIC  32
@@ -111,6 +115,7 @@ typedef struct be_state {
   double* total_dist;   /* (N)  f64                               total_distance    */
   double* ep_return;    /* (N)  f64                               total_reward_accumulated */
   int32_t* ep_len;      /* (N)  steps since reset (TimeLimit elapsed; also the obstacles' curr_counter phase) */
+  uint32_t* episode;    /* (N)  resets so far; with ep_len it keys this env's Philox draws */
   int32_t* static_obs;  /* (Ns, N) int16x2 packed                 static_obstacle_list */
   int32_t* dyn_obs;     /* (Nd, N) int16x2 packed                 dynamic_obstacle_list */
   uint8_t* dyn_goal;    /* (Nd, N) index into goals               obstacle.curr_goal */
@@ -148,7 +153,8 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out);
 int be_destroy(be_ctx* ctx);
 
 /* Reset envs (all, or those with mask[i] != 0) and write the obs of every env.
- * reset_tape == NULL: draws come from Philox(seed; global env id, reset epoch).
+ * A reset env's episode counter is incremented first.
+ * reset_tape == NULL: draws come from Philox(seed; global env id, new episode).
  * reset_tape != NULL: (tape_len, N) int16, the randint values the reference's
  * reset() would consume, in call order (parity mode).                           */
 int be_reset(be_ctx* ctx, const be_state* st, const uint8_t* mask,
@@ -170,12 +176,8 @@ int be_observe(be_ctx* ctx, const be_state* st, const be_out* out, void* stream)
  * by (seed, global env id): identical per global env at any GPU count.         */
 int be_sample_actions(be_ctx* ctx, uint8_t* actions_out, int32_t steps, uint64_t seed, void* stream);
 
-/* Synchronise the context's stream work and read (then clear) the device status word. */
+/* Synchronise the stream and read (then clear) the device status word. */
 int be_status(be_ctx* ctx, int32_t* status_out, void* stream);
-
-/* Number of be_step calls issued (device step counter keys the Philox stream). */
-int be_get_step_counter(be_ctx* ctx, uint64_t* value, void* stream);
-int be_set_step_counter(be_ctx* ctx, uint64_t value, void* stream);
 
 #ifdef __cplusplus
 }

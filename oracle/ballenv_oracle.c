@@ -40,8 +40,12 @@
 #define PHILOX_W0 0x9E3779B9u
 #define PHILOX_W1 0xBB67AE85u
 
-enum { PURPOSE_STEP_OBS = 1, PURPOSE_ACTION = 2, PURPOSE_AUTORESET = 3, PURPOSE_RESET = 4,
-       PURPOSE_SAMPLE = 5 };
+/* counter = (global env id, c1, c2, purpose << 24 | sub):
+ *   obstacle moves  c1 = episode, c2 = ep_len before the step, sub = obstacle >> 1
+ *   sampled action  c1 = episode, c2 = ep_len before the step, sub = 0
+ *   reset draw k    c1 = the new episode number, c2 = 0, sub = k >> 2 (word k & 3)
+ *   be_sample_actions: c1 = t, c2 = 0                                              */
+enum { PURPOSE_STEP_OBS = 1, PURPOSE_ACTION = 2, PURPOSE_RESET = 3, PURPOSE_SAMPLE = 4 };
 
 static void philox4x32_10(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
   uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
@@ -58,10 +62,10 @@ static void philox4x32_10(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, ui
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-/* word w of the Philox block for (env gid, step, purpose, sub) */
-static uint32_t philox_word(uint64_t seed, uint32_t gid, uint64_t step, uint32_t purpose,
+/* word w of the Philox block for (env gid, c1, c2, purpose, sub) */
+static uint32_t philox_word(uint64_t seed, uint32_t gid, uint32_t c1, uint32_t c2, uint32_t purpose,
                             uint32_t sub, int w) {
-  uint32_t ctr[4] = {gid, (uint32_t)step, (uint32_t)(step >> 32), (purpose << 24) | (sub & 0xFFFFFFu)};
+  uint32_t ctr[4] = {gid, c1, c2, (purpose << 24) | (sub & 0xFFFFFFu)};
   uint32_t out[4];
   philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), out);
   return out[w & 3];
@@ -99,7 +103,7 @@ static int check_overlap_rect(const be_config* c, int32_t x1, int32_t y1, int32_
 typedef struct {
   const be_config* c;
   const int16_t* tape; int32_t tape_len; int32_t n; int32_t env; int32_t cursor;
-  uint64_t seed; uint32_t gid; uint64_t step; uint32_t purpose;
+  uint64_t seed; uint32_t gid; uint32_t c1, c2; uint32_t purpose;
   int32_t* status;
 } draw_src;
 
@@ -110,7 +114,7 @@ static int32_t draw(draw_src* s, int32_t lo, int32_t hi) {
     if (k >= s->tape_len) { *s->status |= BE_STATUS_RESET_TAPE_EXHAUSTED; return lo; }
     return s->tape[(int64_t)k * s->n + s->env];
   }
-  return map_range(philox_word(s->seed, s->gid, s->step, s->purpose, (uint32_t)k >> 2, k & 3), lo, hi);
+  return map_range(philox_word(s->seed, s->gid, s->c1, s->c2, s->purpose, (uint32_t)k >> 2, k & 3), lo, hi);
 }
 
 #define REJECT_LIMIT 4096
@@ -135,6 +139,7 @@ static void reset_env(const be_config* c, const be_state* st, int32_t i, draw_sr
   st->prev_dist[i] = dist;                                             /* state[2] = pre-resample dist (Q9) */
   st->ep_return[i] = 0.0;                                              /* :129 */
   st->ep_len[i] = 0;
+  st->episode[i] = ds->c1;                                             /* new episode number */
   for (int32_t k = 0; k < c->num_static; ++k) {                        /* :131-149 */
     int32_t ox = 0, oy = 0; guard = 0;
     for (;;) {
@@ -241,11 +246,11 @@ int orc_observe(const be_config* c, const be_state* st, const be_out* out) {
 }
 
 int orc_reset(const be_config* c, const be_state* st, const uint8_t* mask, const int16_t* tape,
-              int32_t tape_len, const be_out* out, uint64_t step_counter, int32_t* status) {
+              int32_t tape_len, const be_out* out, int32_t* status) {
   for (int32_t i = 0; i < c->num_envs; ++i) {
     if (mask && !mask[i]) continue;
     draw_src ds = {c, tape, tape_len, c->num_envs, i, 0, c->seed,
-                   (uint32_t)(c->env_offset + i), step_counter, PURPOSE_RESET, status};
+                   (uint32_t)(c->env_offset + i), st->episode[i] + 1u, 0u, PURPOSE_RESET, status};
     reset_env(c, st, i, &ds);
   }
   if (out && out->obs) orc_observe(c, st, out);
@@ -259,11 +264,11 @@ static void stats_add(double* s, double ret, int32_t len) {
 }
 
 int orc_step(const be_config* c, const be_state* st, const uint8_t* actions,
-             const int16_t* deltas, const int16_t* tape, const be_out* out,
-             uint64_t step_counter, int32_t* status) {
+             const int16_t* deltas, const int16_t* tape, const be_out* out, int32_t* status) {
   const int32_t N = c->num_envs, F = 4 + c->window * c->window;
   for (int32_t i = 0; i < N; ++i) {
     uint32_t gid = (uint32_t)(c->env_offset + i);
+    uint32_t episode = st->episode[i], len0 = (uint32_t)st->ep_len[i];
     int32_t dx, dy;
     if (actions) {
       int32_t a = actions[i];
@@ -272,7 +277,7 @@ int orc_step(const be_config* c, const be_state* st, const uint8_t* actions,
     } else if (deltas) {
       dx = deltas[2 * (int64_t)i]; dy = deltas[2 * (int64_t)i + 1];
     } else {
-      int32_t a = map_range(philox_word(c->seed, gid, step_counter, PURPOSE_ACTION, 0, 0), 0, c->num_actions);
+      int32_t a = map_range(philox_word(c->seed, gid, episode, len0, PURPOSE_ACTION, 0, 0), 0, c->num_actions);
       dx = c->actions[a][0]; dy = c->actions[a][1];
     }
     double old_dist = st->prev_dist[i];                                /* :236 */
@@ -288,7 +293,7 @@ int orc_step(const be_config* c, const be_state* st, const uint8_t* actions,
       /* tape: rows (k*2 + d, N) of this step's (Nd, 2, N) tape.
        * Philox: draw d of obstacle k is word 2*(k&1)+d of block sub=k>>1, i.e. cursor 2k+d. */
       draw_src ds = {c, tape ? tape + (int64_t)k * 2 * N : NULL, 2, N, i, tape ? 0 : 2 * k,
-                     c->seed, gid, step_counter, PURPOSE_STEP_OBS, status};
+                     c->seed, gid, episode, len0, PURPOSE_STEP_OBS, status};
       move_obstacle(c, st, i, k, counter, &ds);
     }
     int32_t gx = pk_x(st->goal[i]), gy = pk_y(st->goal[i]);
@@ -323,7 +328,7 @@ int orc_step(const be_config* c, const be_state* st, const uint8_t* actions,
       if (out->stats) stats_add(out->stats, st->ep_return[i], len);
       if (c->autoreset) {
         if (out->terminal_obs) observe_env(c, st, i, out->terminal_obs + (int64_t)i * F);
-        draw_src ds = {c, NULL, 0, N, i, 0, c->seed, gid, step_counter, PURPOSE_AUTORESET, status};
+        draw_src ds = {c, NULL, 0, N, i, 0, c->seed, gid, episode + 1u, 0u, PURPOSE_RESET, status};
         reset_env(c, st, i, &ds);
       }
     }
@@ -341,7 +346,7 @@ int orc_sample_actions(const be_config* c, uint8_t* out, int32_t steps, uint64_t
   for (int32_t t = 0; t < steps; ++t)
     for (int32_t i = 0; i < c->num_envs; ++i)
       out[(int64_t)t * c->num_envs + i] = (uint8_t)map_range(
-          philox_word(seed, (uint32_t)(c->env_offset + i), (uint64_t)t, PURPOSE_SAMPLE, 0, 0), 0,
+          philox_word(seed, (uint32_t)(c->env_offset + i), (uint32_t)t, 0u, PURPOSE_SAMPLE, 0, 0), 0,
           c->num_actions);
   return 0;
 }

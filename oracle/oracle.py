@@ -15,7 +15,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.realpath(__file__))
 SO = os.path.join(HERE, "liboracle.so")
-STATE_KEYS = ("agent", "goal", "prev_dist", "total_dist", "ep_return", "ep_len", "static_obs", "dyn_obs", "dyn_goal")
+STATE_KEYS = ("agent", "goal", "prev_dist", "total_dist", "ep_return", "ep_len", "episode", "static_obs", "dyn_obs",
+              "dyn_goal")
 
 
 def build(force: bool = False) -> str:
@@ -35,8 +36,8 @@ def lib():
         build()
         L = C.CDLL(SO)
         vp, i32, u64 = C.c_void_p, C.c_int32, C.c_uint64
-        L.orc_step.argtypes = [vp, vp, vp, vp, vp, vp, u64, vp]
-        L.orc_reset.argtypes = [vp, vp, vp, vp, i32, vp, u64, vp]
+        L.orc_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.orc_reset.argtypes = [vp, vp, vp, vp, i32, vp, vp]
         L.orc_observe.argtypes = [vp, vp, vp]
         L.orc_sample_actions.argtypes = [vp, vp, i32, u64]
         L.orc_philox4x32_10.argtypes = [vp, C.c_uint32, C.c_uint32, vp]
@@ -53,7 +54,7 @@ def new_state(cfg, n=None):
     ns, nd = max(cfg.num_static, 1), max(cfg.num_dynamic, 1)
     return dict(agent=np.zeros((n, 2), np.int16), goal=np.zeros((n, 2), np.int16),
                 prev_dist=np.zeros(n), total_dist=np.zeros(n), ep_return=np.zeros(n),
-                ep_len=np.zeros(n, np.int32), static_obs=np.zeros((ns, n, 2), np.int16),
+                ep_len=np.zeros(n, np.int32), episode=np.zeros(n, np.uint32), static_obs=np.zeros((ns, n, 2), np.int16),
                 dyn_obs=np.zeros((nd, n, 2), np.int16), dyn_goal=np.zeros((nd, n), np.uint8))
 
 
@@ -81,18 +82,18 @@ def _out_struct(o):
                  _p(o.get("final_len")), _p(o.get("stats")))
 
 
-def step(cfg, st, out, actions=None, deltas=None, tape=None, step_counter=0):
+def step(cfg, st, out, actions=None, deltas=None, tape=None):
     status = C.c_int32(0)
     lib().orc_step(C.byref(cfg), C.byref(_state_struct(st)), _p(actions), _p(deltas), _p(tape),
-                   C.byref(_out_struct(out)), int(step_counter), C.byref(status))
+                   C.byref(_out_struct(out)), C.byref(status))
     return status.value
 
 
-def reset(cfg, st, out, mask=None, tape=None, step_counter=0):
+def reset(cfg, st, out, mask=None, tape=None):
     status = C.c_int32(0)
     L = 0 if tape is None else tape.shape[0]
     lib().orc_reset(C.byref(cfg), C.byref(_state_struct(st)), _p(mask), _p(tape), L,
-                    C.byref(_out_struct(out)) if out is not None else None, int(step_counter), C.byref(status))
+                    C.byref(_out_struct(out)) if out is not None else None, C.byref(status))
     return status.value
 
 

@@ -50,7 +50,7 @@ def init_state(fx, prefix="init_"):
               prev_dist=fx[prefix + "prev_dist"].astype(np.float64).copy(),
               total_dist=fx[prefix + "total_dist"].astype(np.float64).copy(), ep_return=np.zeros(E),
               ep_len=(fx[prefix + "ep_len"].astype(np.int32).copy() if prefix + "ep_len" in fx
-                      else np.zeros(E, np.int32)))
+                      else np.zeros(E, np.int32)), episode=np.ones(E, np.uint32))
     s = fx[prefix + "static"]
     d = fx[prefix + "dyn"]
     st["static_obs"] = np.ascontiguousarray(s.transpose(1, 0, 2).astype(np.int16)) if s.shape[1] else np.zeros((1, E, 2), np.int16)
@@ -75,4 +75,5 @@ def window_state(agent, goal, obst, nobs, far=-20000):
             so[:k, i] = obst[i, :k]
     return dict(agent=agent.astype(np.int16).copy(), goal=goal.astype(np.int16).copy(), prev_dist=np.zeros(n),
                 total_dist=np.ones(n), ep_return=np.zeros(n), ep_len=np.zeros(n, np.int32),
+                episode=np.zeros(n, np.uint32),
                 static_obs=so, dyn_obs=np.zeros((1, n, 2), np.int16), dyn_goal=np.zeros((1, n), np.uint8)), K

@@ -1,0 +1,200 @@
+"""CPU tests: the C-ABI library loads and exports what include/ballenv.h
+declares; host-side config / sharding / stats logic (no compute calls)."""
+import ctypes as C
+import os
+import re
+import subprocess
+import sys
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from gym_ballenv_amd import _abi
+from gym_ballenv_amd.config import EnvConfig, MOVE_LIST
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "ballenv.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(be_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _abi.lib()
+    declared = header_functions()
+    assert declared, "no functions parsed from the header"
+    assert sorted(_abi.EXPORTS) == declared
+    for name in declared:
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    for name in declared:
+        assert re.search(rf"\bT {name}\b", out), f"{name} not exported"
+    assert L.be_abi_version() == _abi.ABI_VERSION
+
+
+def test_library_is_gfx950():
+    blob = open(_abi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob       # the embedded code object targets gfx950
+
+
+def test_config_struct_layout_matches_header():
+    # offsets the C compiler picks for be_config (checked with a tiny C program)
+    src = os.path.join(ROOT, "include")
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "ballenv.h"
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(be_config), offsetof(be_config, threshold_goal),
+  offsetof(be_config, goals), offsetof(be_config, actions), offsetof(be_config, autoreset), sizeof(be_state),
+  sizeof(be_out)); return 0;}'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        cfile, exe = os.path.join(d, "t.c"), os.path.join(d, "t")
+        open(cfile, "w").write(prog)
+        subprocess.run(["gcc", "-I", src, cfile, "-o", exe], check=True)
+        got = [int(v) for v in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    want = [C.sizeof(_abi.BeConfig), _abi.BeConfig.threshold_goal.offset, _abi.BeConfig.goals.offset,
+            _abi.BeConfig.actions.offset, _abi.BeConfig.autoreset.offset, C.sizeof(_abi.BeState),
+            C.sizeof(_abi.BeOut)]
+    assert got == want
+
+
+def test_defaults_match_reference():
+    c = _abi.default_config(65536, 10)
+    py = EnvConfig().to_abi(65536, 10)
+    assert bytes(c) == bytes(py)
+    assert c.num_static == 13 and c.num_dynamic == 5 and c.goal_change_step == 50 and c.obs_certainty == 60
+    assert c.dynamic_penalty == 8000.0 and c.static_penalty == 1.0 and c.time_limit == 1000
+    assert [tuple(c.actions[a]) for a in range(c.num_actions)] == MOVE_LIST
+    assert _abi.step_bytes(c) == 74 + 4 * 13 + 9 * 5 + 104   # 275 B / env-step at W=10
+    assert _abi.config_check(c) == ""
+
+
+@pytest.mark.parametrize("field,value,msg", [
+    ("window", 0, "window"), ("window", 65, "window"), ("num_static", 65, "num_static"),
+    ("num_envs", 0, "num_envs"), ("speed_x", 0, "speeds"), ("num_actions", 0, "num_actions"),
+    ("radius_obstacle", 5000, "radii"), ("time_limit", -1, "time_limit")])
+def test_config_check_rejects(field, value, msg):
+    c = _abi.default_config(16, 5)
+    setattr(c, field, value)
+    assert msg in _abi.config_check(c)
+
+
+def test_config_needs_goal_per_dynamic_obstacle():
+    c = EnvConfig(num_dynamic=6, obstacle_speed=[1] * 6)
+    with pytest.raises(ValueError, match="goal per dynamic"):
+        c.validate(8, 5)
+
+
+def test_from_args_mirrors_customize_environment():
+    args = SimpleNamespace(static_obstacles=7, dynamic_obstacles=2, obstacle_speed=["2", 3],
+                           obs_goal_position=["1,2", " 30,40 "], time_step_for_change=9, rd_th_obs=33,
+                           rd_th_agent=80, static_thresholds=[0, 0], dynamic_thresholds=[10, 10],
+                           static_penalty=[5, 6], dynamic_penalty=[7, 9000])
+    c = EnvConfig.from_args(args)
+    assert (c.num_static, c.num_dynamic, c.obstacle_speed, c.goals) == (7, 2, [2, 3], [(1, 2), (30, 40)])
+    assert (c.goal_change_step, c.obs_certainty, c.static_penalty, c.dynamic_penalty) == (9, 33, 6.0, 9000.0)
+    bad = SimpleNamespace(**{**vars(args), "obstacle_speed": [1]})
+    with pytest.raises(AssertionError):
+        EnvConfig.from_args(bad)
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    ctx = C.c_void_p()
+    c = _abi.default_config(16, 5)
+    rc = _abi.lib().be_create(C.byref(c), 0, C.byref(ctx))
+    assert rc != 0 and not ctx.value
+    assert _abi.lib().be_last_error(None)
+
+
+def test_batched_env_refuses_cpu():
+    import gym_ballenv_amd as gb
+    with pytest.raises(ValueError, match="GPU"):
+        gb.BatchedBallEnv(4, 5, device="cpu")
+
+
+def test_shard():
+    from gym_ballenv_amd.distributed import shard
+    for total, world in ((262144, 8), (10, 3), (7, 8)):
+        parts = [shard(total, r, world) for r in range(world)]
+        assert sum(n for _, n in parts) == total
+        off = 0
+        for o, n in parts:
+            assert o == off
+            off += n
+
+
+def test_combine_stats():
+    import torch
+    from gym_ballenv_amd.distributed import combine_stats
+    a = torch.tensor([[2, -3.0, 5.0, 10, -2.0, -1.0, 0, 0], [1, 4.0, 16.0, 7, 4.0, 4.0, 0, 0]], dtype=torch.float64)
+    d = combine_stats(a)
+    assert d["episodes"] == 3 and d["sum_return"] == 1.0 and d["min_return"] == -2.0 and d["max_return"] == 4.0
+    assert abs(d["mean_length"] - 17 / 3) < 1e-12
+
+
+GLOO_WORKER = r'''
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"])
+from gym_ballenv_amd.distributed import shard, gather_stats, combine_stats
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+off, n = shard(262144, r, w)
+s = torch.tensor([r + 1.0, 10.0 * (r + 1), 0, 5.0, -float(r), float(r), 0, 0], dtype=torch.float64)
+g = gather_stats(s)
+d = combine_stats(g)
+assert g.shape == (w, 8) and d["episodes"] == sum(range(1, w + 1)), d
+assert d["min_return"] == -(w - 1) and d["max_return"] == w - 1
+offs = [torch.zeros(2, dtype=torch.int64) for _ in range(w)]
+dist.all_gather(offs, torch.tensor([off, n]))
+assert sum(int(o[1]) for o in offs) == 262144
+dist.destroy_process_group()
+print("ok", r)
+'''
+
+
+def test_gloo_world_size_2(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text(GLOO_WORKER)
+    env = dict(os.environ, ROOT=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29533", str(script)]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.count("ok") == 2
+
+
+def test_python_port_matches_golden_subset():
+    """The CPU-baseline port (oracle/py_ballenv.py) reproduces the reference on golden episodes."""
+    from helpers import load
+    from oracle.py_ballenv import PyBallEnv, MOVE_LIST as ML
+    fx = load("rollouts_directed")
+    E, T = fx["actions"].shape
+    for e in range(2):
+        env = PyBallEnv()
+        env.set_state(fx["init_agent"][e], fx["init_goal"][e], fx["init_prev_dist"][e], fx["init_total_dist"][e],
+                      fx["init_static"][e], fx["init_dyn"][e], fx["init_dyn_goal"][e])
+        assert env.prep_state4(env.state, 10) == list(fx["init_obs10"][e])
+        for t in range(200):
+            draws = [[int(v) for v in fx["tape"][e, t, k] if v >= 0] for k in range(5)]
+            state, r, d = env.step(ML[fx["actions"][e, t]], draws_per_obstacle=draws)
+            assert r == fx["reward"][e, t] and d == bool(fx["done"][e, t]), (e, t)
+            assert env.prep_state4(state, 5) == list(fx["obs5"][e, t]), (e, t)
+
+
+def test_python_port_resets_match_golden():
+    from helpers import load
+    from oracle.py_ballenv import PyBallEnv, _Draws
+    fx = load("resets")
+    for e in range(50):
+        env = PyBallEnv()
+        env.reset(_Draws([int(v) for v in fx["default_tape"][e] if v >= 0]))
+        assert env.state[0] == tuple(fx["default_agent"][e])
+        assert env.state[2] == fx["default_prev_dist"][e]
+        assert [tuple(p) for p in env.static] == [tuple(p) for p in fx["default_static"][e]]

@@ -12,7 +12,8 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-KEYS = ("agent", "goal", "prev_dist", "total_dist", "ep_return", "ep_len", "static_obs", "dyn_obs", "dyn_goal")
+KEYS = ("agent", "goal", "prev_dist", "total_dist", "ep_return", "ep_len", "episode", "static_obs", "dyn_obs",
+        "dyn_goal")
 
 
 def make_env(cfg_py, n, W, dev, seed=0xBA11, env_offset=0, **kw):
@@ -25,7 +26,9 @@ def load_np_state(env, st):
 
 
 def np_state(env):
-    return {k: getattr(env, k).cpu().numpy().copy() for k in KEYS}
+    d = {k: getattr(env, k).cpu().numpy().copy() for k in KEYS}
+    d["episode"] = d["episode"].view(np.uint32)
+    return d
 
 
 def assert_state_equal(env, st, msg=""):
@@ -192,14 +195,14 @@ def test_vs_oracle_philox_autoreset(gpu, W, N):
     env = make_env(cfg_py, N, W, gpu, seed=77, terminal_obs=True)
     st = oracle.new_state(cfg)
     out = oracle.new_out(cfg, terminal=True)
-    oracle.reset(cfg, st, out, step_counter=0)
+    oracle.reset(cfg, st, out)
     np.testing.assert_array_equal(env.reset().cpu().numpy(), out["obs"])
     assert_state_equal(env, st, "reset")
     steps = 60 if N <= 4096 else 12
     for t in range(steps):
         out["terminal_obs"][:] = 0
         env.terminal_obs.zero_()
-        oracle.step(cfg, st, out, step_counter=1 + t)
+        oracle.step(cfg, st, out)
         obs, reward, done, info = env.step()
         d = done.cpu().numpy()
         np.testing.assert_array_equal(reward.cpu().numpy(), out["reward"], err_msg=f"t={t}")
@@ -214,7 +217,6 @@ def test_vs_oracle_philox_autoreset(gpu, W, N):
     s_orc = out["stats"]
     assert s_gpu[0] == s_orc[0] and s_gpu[4] == s_orc[4] and s_gpu[5] == s_orc[5] and s_gpu[3] == s_orc[3]
     np.testing.assert_allclose(s_gpu[1:3], s_orc[1:3], rtol=1e-12, atol=1e-9)
-    assert env.step_counter == 1 + steps
     env.status()
     env.close()
 
@@ -250,7 +252,7 @@ def test_distance_sqrt_exhaustive(gpu):
     env = make_env(cfg_py, N, 3, gpu)
     st = {"agent": np.stack([xs.ravel(), ys.ravel()], 1).astype(np.int16),
           "goal": np.zeros((N, 2), np.int16), "prev_dist": np.zeros(N), "total_dist": np.ones(N),
-          "ep_return": np.zeros(N), "ep_len": np.zeros(N, np.int32),
+          "ep_return": np.zeros(N), "ep_len": np.zeros(N, np.int32), "episode": np.zeros(N, np.uint32),
           "static_obs": np.zeros((1, N, 2), np.int16), "dyn_obs": np.zeros((1, N, 2), np.int16),
           "dyn_goal": np.zeros((1, N), np.uint8)}
     load_np_state(env, st)
@@ -271,10 +273,10 @@ def test_large_batch_subset_vs_oracle(gpu):
     cfg = cfg_py.to_abi(k, W, env_offset=a, seed=11)
     st = oracle.new_state(cfg)
     out = oracle.new_out(cfg)
-    oracle.reset(cfg, st, out, step_counter=0)
+    oracle.reset(cfg, st, out)
     for t in range(12):
         obs, reward, done, _ = env.step()
-        oracle.step(cfg, st, out, step_counter=1 + t)
+        oracle.step(cfg, st, out)
         np.testing.assert_array_equal(obs[a:a + k].cpu().numpy(), out["obs"])
         np.testing.assert_array_equal(reward[a:a + k].cpu().numpy(), out["reward"])
     # global invariants on the whole batch

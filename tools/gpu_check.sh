@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace of the bench.
+# Every GPU step has its own time limit; a crash/timeout stops the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc"
+  if [ $rc -gt 1 ]; then echo "stopping after $name (rc=$rc)"; tail -20 "gpurun_out/$name.log"; exit $rc; fi
+  return 0
+}
+TAG=${TAG:-run}
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+  step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -o timeout=300
+  tail -3 gpurun_out/pytest_gpu.log
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+step bench 400 python bench.py ${BENCH_ARGS:-}
+tail -1 gpurun_out/bench.log
+if [ "${PROFILE:-1}" = "1" ]; then
+  step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
+      python bench.py --no-cpu-baseline --steps 300 --warmup 20 ${BENCH_ARGS:-}
+  find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \;
+fi
