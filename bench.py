@@ -149,7 +149,7 @@ def main():
         el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
-        per_rank = gb.gather_stats(env.stats_buf)            # RCCL all_gather of episode returns
+        per_rank = gb.gather_stats(env.stats_record())            # RCCL all_gather of episode returns
         ep = gb.combine_stats(per_rank)
     else:
         ep = env.episode_stats()

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_STATIC, MAX_DYNAMIC, MAX_GOALS, MAX_ACTIONS, MAX_WINDOW = 64, 32, 16, 16, 64
 
 BE_OK, BE_E_INVALID, BE_E_HIP, BE_E_NOMEM, BE_E_DEVICE = 0, -1, -2, -3, -4
@@ -21,7 +21,8 @@ LIB_NAME = "libballenv.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.realpath(__file__)), LIB_NAME)
 
 # Names declared in include/ballenv.h (checked by tests/test_abi.py).
-EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_bytes", "be_last_error",
+EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_bytes", "be_stats_slots",
+           "be_last_error",
            "be_create", "be_destroy", "be_reset", "be_step", "be_observe", "be_sample_actions",
            "be_status")
 
@@ -80,6 +81,7 @@ def lib() -> C.CDLL:
         "be_config_default": (C.c_int, [P(BeConfig), i32, i32]),
         "be_config_check": (C.c_int, [P(BeConfig), C.c_char_p, i32]),
         "be_step_bytes": (i64, [P(BeConfig)]),
+        "be_stats_slots": (i64, [P(BeConfig)]),
         "be_last_error": (C.c_char_p, [vp]),
         "be_create": (C.c_int, [P(BeConfig), i32, P(vp)]),
         "be_destroy": (C.c_int, [vp]),
@@ -120,3 +122,7 @@ def config_check(c: BeConfig) -> str:
 
 def step_bytes(c: BeConfig) -> int:
     return int(lib().be_step_bytes(C.byref(c)))
+
+
+def stats_slots(c: BeConfig) -> int:
+    return int(lib().be_stats_slots(C.byref(c)))

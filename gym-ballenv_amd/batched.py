@@ -83,7 +83,7 @@ class BatchedBallEnv:
         self.final_return = z(N, dt=torch.float64)
         self.final_len = z(N, dt=torch.int32)
         self.terminal_obs = z(N, F, dt=torch.uint8) if self._want_terminal else None
-        self.stats_buf = z(8, dt=torch.float64)
+        self.stats_buf = z(_abi.stats_slots(cfg.to_abi(N, self.window)), 8, dt=torch.float64)
         self.clear_stats()
         self._st = _abi.BeState(*[getattr(self, k).data_ptr() for k in self.STATE_KEYS])
         self._out = _abi.BeOut(self.obs.data_ptr(), _ptr(self.obs_f32), self.reward.data_ptr(),
@@ -203,11 +203,19 @@ class BatchedBallEnv:
 
     def clear_stats(self) -> None:
         self.stats_buf.zero_()
-        self.stats_buf[4] = math.inf
-        self.stats_buf[5] = -math.inf
+        self.stats_buf[:, 4] = math.inf
+        self.stats_buf[:, 5] = -math.inf
+
+    def stats_record(self) -> torch.Tensor:
+        """(8,) f64 on the device: the per-block slots reduced (sums add, min/max reduce)."""
+        b = self.stats_buf
+        r = b.sum(0)
+        r[4] = b[:, 4].min()
+        r[5] = b[:, 5].max()
+        return r
 
     def episode_stats(self) -> dict:
-        s = self.stats_buf.cpu().tolist()
+        s = self.stats_record().cpu().tolist()
         n = s[0]
         return {"episodes": int(n), "mean_return": s[1] / n if n else float("nan"),
                 "sum_return": s[1], "sum_return_sq": s[2], "mean_length": s[3] / n if n else float("nan"),

@@ -10,11 +10,19 @@
 //   prep_state4(state, W)             examples/ball_cnn_ac3.py:384-412 (+ prep_state2 :330-352)
 // and, with autoreset, BallEnv.reset  ballenv_env.py:113-167 for the envs that finished.
 //
-// Memory: every per-env word the step needs is loaded up front (obstacles in
-// register chunks of 16 static / 8 dynamic), so a wave has ~30 independent
-// loads in flight instead of a chain of dependent HBM round trips.  There is
-// no cross-block communication at all: randomness is Philox keyed by per-env
-// state (global env id, episode, ep_len), so no global counter or atomics.
+// Latency structure (at 65536 envs there is one wave per SIMD, so every
+// dependent round trip is exposed):
+//  * the kernel argument block is small and hot-first (KParams, 4 cache
+//    lines): scalar loads from the kernarg segment that miss are each a full
+//    round trip, and a big by-value config struct spread them over the kernel;
+//  * everything indexed per lane or used only on cold paths (goal/action
+//    tables, obstacle speeds, spawn strips) lives in a device buffer staged
+//    into LDS once per block;
+//  * every per-env word the step needs is loaded up front (obstacles in
+//    register chunks of 16 static / 8 dynamic), so all of a wave's loads are in
+//    flight together and one barrier covers them and the table staging;
+//  * no cross-block communication: randomness is Philox keyed by per-env state
+//    (global env id, episode, ep_len), so there is no global counter or atomic.
 //
 // Window ("feature extraction") stage: an obstacle can only light cells of a
 // W x W window if its radius-R disk meets the window's cell box.  Pass 1 tests
@@ -36,6 +44,7 @@
 #include <new>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "ballenv.h"
@@ -50,27 +59,62 @@ constexpr int CD = 8;   // dynamic obstacles per register chunk
 
 enum Mode { MODE_STEP = 0, MODE_RESET = 1, MODE_OBSERVE = 2 };
 
-// Host-precomputed lookup tables (read from the kernarg segment).
+// Per-context tables: a device buffer staged into LDS once per block.
 struct Tables {
   int32_t goal[BE_MAX_GOALS];                 // packed goal xy
   int32_t action[BE_MAX_ACTIONS];             // packed (dx, dy)
+  int32_t speed[BE_MAX_DYNAMIC];              // obstacle_speed
+  int32_t strip_obs_x, strip_obs_y, strip_goal_x, strip_goal_y, strip_agent_x, strip_agent_y;
+  int32_t radius_obstacle, radius_agent;
   uint8_t n_other[BE_MAX_GOALS];              // goals with a different value than goal g
   uint8_t other[BE_MAX_GOALS][BE_MAX_GOALS];  // pick -> goal index, per current goal g (newGoalList)
 };
 
-struct KArgs {
-  be_config c;
-  Tables t;
-  be_state st;
-  be_out out;
-  const uint8_t* actions;
-  const int16_t* deltas;
-  const int16_t* tape;        // (Nd, 2, N) step draw tape or NULL
-  const uint8_t* mask;        // reset mask or NULL
-  const int16_t* reset_tape;  // (L, N) or NULL
-  int32_t reset_tape_len;
+// Kernel arguments: hot fields first, 64-byte lines (see the latency notes above).
+struct KParams {
+  // line 0
+  int32_t* agent; int32_t* goal; double* prev_dist; double* total_dist;
+  double* ep_return; int32_t* ep_len; uint32_t* episode; int32_t* static_obs;
+  // line 1
+  int32_t* dyn_obs; uint8_t* dyn_goal; uint8_t* obs; float* obs_f32;
+  double* reward; uint8_t* done; const uint8_t* actions; const Tables* tables;
+  // line 2
+  int32_t n, window, ns, nd, R, speed_x, speed_y, screen_w;
+  int32_t screen_h, goal_change, certainty, time_limit, num_actions, autoreset, gid0, dbg;
+  // line 3
+  double threshold_goal, time_penalty, static_penalty, dynamic_penalty, min_spawn_dist;
+  double inv_g1;               // 1 / (goal_change + 1): counter = ep_len mod (G+1) without an integer divide
+  unsigned long long seed;
   int* status;
+  // line 4 (cold)
+  const int16_t* deltas; const int16_t* tape; const uint8_t* mask; const int16_t* reset_tape;
+  uint8_t* truncated; uint8_t* terminal_obs; double* final_return; int32_t* final_len;
+  // line 5 (cold)
+  double* stats;               // (slots, 8): one slot per block of the step kernel (be_stats_slots)
+  int32_t reset_tape_len;
 };
+
+// Diagnostic phase-skip bits (timing ablations only; outputs are wrong when set).
+enum : uint32_t { DBG_NO_STATS = 1, DBG_NO_RASTER = 2, DBG_NO_OBS = 4, DBG_NO_PHILOX = 8, DBG_NO_DYN = 16,
+                  DBG_NO_NEAR = 32, DBG_EXIT_ENTRY = 64, DBG_EXIT_BARRIER = 128, DBG_EXIT_PHYSICS = 256,
+                  DBG_EXIT_RASTER = 512 };
+
+// Diagnostics-only build (-DBE_DIAG_STAMPS): per-wave phase stamps for tools/microbench.
+#ifdef BE_DIAG_STAMPS
+constexpr int DIAG_WAVES = 1 << 16, DIAG_POINTS = 12;
+__device__ unsigned long long g_diag_rt[DIAG_WAVES][DIAG_POINTS];   // s_memrealtime (100 MHz, chip-wide)
+__device__ unsigned long long g_diag_cy[DIAG_WAVES][DIAG_POINTS];   // s_memtime (shader clock)
+__device__ __forceinline__ void diag_stamp(int point) {
+  const int w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+  if ((threadIdx.x & 63) == 0 && w < DIAG_WAVES) {
+    g_diag_rt[w][point] = __builtin_amdgcn_s_memrealtime();
+    g_diag_cy[w][point] = __builtin_amdgcn_s_memtime();
+  }
+}
+#define DIAG(pt) diag_stamp(pt)
+#else
+#define DIAG(pt) ((void)0)
+#endif
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ int px(int32_t p) { return (int)(int16_t)(p & 0xFFFF); }
@@ -143,25 +187,25 @@ struct Win {
   int w;          // W
   int kr;         // distinct rows K = max(W-1, 1)
   int R, R2;
-  __device__ Win(const be_config& c, int ax, int ay) {
-    w = c.window; int h = w / 2;
-    sx = c.speed_x; sy = c.speed_y;
+  __device__ Win(const KParams& p, int ax, int ay) {
+    w = p.window; const int h = w / 2;
+    sx = p.speed_x; sy = p.speed_y;
     x0 = ax - sx * h; y0 = ay - sy * h;
     kr = w > 1 ? w - 1 : 1;
-    R = c.radius_obstacle + c.radius_agent; R2 = R * R;
+    R = p.R; R2 = R * R;
   }
   // Can obstacle (ox,oy) light any cell?  (f, e) = its window-relative position.
   __device__ __forceinline__ bool near(int ox, int oy, int& f, int& e) const {
     f = ox - x0; e = oy - y0;
-    int cx = min(max(f, 0), sx * (w - 1));
-    int cy = min(max(e, 0), sy * (kr - 1));
+    const int cx = min(max(f, 0), sx * (w - 1));
+    const int cy = min(max(e, 0), sy * (kr - 1));
     return d2u(f - cx, e - cy) <= (uint32_t)R2;
   }
 };
 
 __device__ __forceinline__ int quadrant(int ax, int ay, int gx, int gy) {
   // prep_state2, examples/ball_cnn_ac3.py:343-351
-  int dx = gx - ax, dy = gy - ay;
+  const int dx = gx - ax, dy = gy - ay;
   if (dx >= 0 && dy >= 0) return 1;
   if (dx < 0 && dy >= 0) return 0;
   if (dx < 0 && dy < 0) return 3;
@@ -177,7 +221,7 @@ struct NearList {
     ++cnt;
   }
   __device__ __forceinline__ void get(int n, int& f, int& e) const {
-    uint32_t v = base[n * BLOCK];
+    const uint32_t v = base[n * BLOCK];
     f = (int)(int16_t)(v & 0xFFFF); e = (int)v >> 16;
   }
 };
@@ -199,9 +243,9 @@ __device__ __forceinline__ void raster_rows(const NearList<BLOCK>& nl, const Win
     nl.get(n, f, e);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      int ady = abs(e - g.sy * k);
+      const int ady = abs(e - g.sy * k);
       if (ady <= g.R) {
-        int hw = isqrt_small(g.R2 - ady * ady);
+        const int hw = isqrt_small(g.R2 - ady * ady);
         int lo, hi;
         if (g.sx == 1) { lo = f - hw; hi = f + hw; }
         else { lo = -floordiv(hw - f, g.sx); hi = floordiv(f + hw, g.sx); }
@@ -247,7 +291,7 @@ __device__ __forceinline__ void stage_row(uint8_t* stage, int tid, const uint32_
 #pragma unroll
     for (int w = 1; w < F / 4; ++w) {
       const int j = 4 * (w - 1);  // first cell of this word (nibble aligned)
-      uint32_t nib = (flat[j >> 5] >> (j & 31)) & 0xFu;
+      const uint32_t nib = (flat[j >> 5] >> (j & 31)) & 0xFu;
       dst[w] = (nib * 0x00204081u) & 0x01010101u;
     }
   } else {
@@ -274,7 +318,7 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid
     float* dst = obs_f32 + row0 * F;
     const int nv = bytes >> 2;
     for (int v = tid; v < nv; v += BLOCK) {
-      uint32_t q = reinterpret_cast<const uint32_t*>(stage)[v];
+      const uint32_t q = reinterpret_cast<const uint32_t*>(stage)[v];
       reinterpret_cast<float4*>(dst)[v] =
           make_float4((float)(q & 0xFF), (float)((q >> 8) & 0xFF), (float)((q >> 16) & 0xFF), (float)(q >> 24));
     }
@@ -290,7 +334,7 @@ __device__ void write_row_generic(const NearList<BLOCK>& nl, const Win& g, int q
     if (rowf) rowf[b] = (float)(b == quad);
   }
   for (int r = 0; r < g.w; ++r) {
-    int k = r > 0 ? r - 1 : 0;
+    const int k = r > 0 ? r - 1 : 0;
     for (int cc = 0; cc < g.w; ++cc) {
       int hit = 0;
       for (int n = 0; n < nl.cnt && !hit; ++n) {
@@ -298,7 +342,7 @@ __device__ void write_row_generic(const NearList<BLOCK>& nl, const Win& g, int q
         nl.get(n, f, e);
         hit = d2u(f - g.sx * cc, e - g.sy * k) <= (uint32_t)g.R2;
       }
-      int b = 4 + r * g.w + cc;
+      const int b = 4 + r * g.w + cc;
       if (row) row[b] = (uint8_t)hit;
       if (rowf) rowf[b] = (float)hit;
     }
@@ -308,79 +352,132 @@ __device__ void write_row_generic(const NearList<BLOCK>& nl, const Win& g, int q
 // ------------------------------------------------------------------ reset
 // BallEnv.reset for one env (ballenv_env.py:113-167); also rebuilds the near list.
 template <int BLOCK>
-__device__ void reset_env(const KArgs& p, int i, ResetDraws& ds, int& ax, int& ay, int& gx, int& gy,
-                          NearList<BLOCK>& nl) {
-  const be_config& c = p.c;
-  const int N = c.num_envs, W = c.screen_width, H = c.screen_height;
-  gx = ds.draw(W - c.strip_goal_x, W);                                  // :115
-  gy = ds.draw(H - c.strip_goal_y, H);                                  // :116
-  ax = ds.draw(0, c.strip_agent_x);                                     // :117
-  ay = ds.draw(0, c.strip_agent_y);                                     // :118
+__device__ void reset_env(const KParams& p, const Tables& t, int i, ResetDraws& ds, int& ax, int& ay, int& gx,
+                          int& gy, NearList<BLOCK>& nl) {
+#ifdef BE_DIAG_NO_RESET
+  (void)p; (void)t; (void)i; (void)ds; ax = ay = gx = gy = 0; nl.cnt = 0; return;
+#endif
+  const int N = p.n, W = p.screen_w, H = p.screen_h;
+  gx = ds.draw(W - t.strip_goal_x, W);                                  // :115
+  gy = ds.draw(H - t.strip_goal_y, H);                                  // :116
+  ax = ds.draw(0, t.strip_agent_x);                                     // :117
+  ay = ds.draw(0, t.strip_agent_y);                                     // :118
   const double dist = calc_dist(gx, gy, ax, ay);                        // :119
-  for (int guard = 0; calc_dist(gx, gy, ax, ay) < c.min_spawn_dist;) {  // :121-126
+  for (int guard = 0; calc_dist(gx, gy, ax, ay) < p.min_spawn_dist;) {  // :121-126
     if (++guard > REJECT_LIMIT) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
-    ax = ds.draw(0, c.strip_agent_x);
-    ay = ds.draw(0, c.strip_agent_y);
+    ax = ds.draw(0, t.strip_agent_x);
+    ay = ds.draw(0, t.strip_agent_y);
   }
-  p.st.agent[i] = pk(ax, ay);
-  p.st.goal[i] = pk(gx, gy);
-  p.st.prev_dist[i] = dist;  // state[2] keeps the pre-resample distance (Q9)
-  p.st.total_dist[i] = calc_dist(ax, ay, gx, gy);                       // :166
-  p.st.ep_return[i] = 0.0;
-  p.st.ep_len[i] = 0;
-  p.st.episode[i] = ds.episode;
-  Win g(c, ax, ay);
+  p.agent[i] = pk(ax, ay);
+  p.goal[i] = pk(gx, gy);
+  p.prev_dist[i] = dist;  // state[2] keeps the pre-resample distance (Q9)
+  p.total_dist[i] = calc_dist(ax, ay, gx, gy);                          // :166
+  p.ep_return[i] = 0.0;
+  p.ep_len[i] = 0;
+  p.episode[i] = ds.episode;
+  const Win g(p, ax, ay);
   nl.cnt = 0;
   // check_overlap_rect (:193-197): |dx| < rad + r_a and |dy| < rad/2 + r_a  <=>  2|dy| < rad + 2 r_a
-  const int rx = c.radius_obstacle + c.radius_agent, ry2 = c.radius_obstacle + 2 * c.radius_agent;
-  for (int k = 0; k < c.num_static; ++k) {                              // :131-149
+  const int rx = t.radius_obstacle + t.radius_agent, ry2 = t.radius_obstacle + 2 * t.radius_agent;
+  for (int k = 0; k < p.ns; ++k) {                                      // :131-149
     int ox = 0, oy = 0;
     for (int guard = 0;;) {
-      ox = ds.draw(c.strip_obs_x, W - c.strip_obs_x);                   // obstacles.__init__ :24-25
-      oy = ds.draw(c.strip_obs_y, H - c.strip_obs_y);
+      ox = ds.draw(t.strip_obs_x, W - t.strip_obs_x);                   // obstacles.__init__ :24-25
+      oy = ds.draw(t.strip_obs_y, H - t.strip_obs_y);
       const bool ra = abs(ox - ax) < rx && 2 * abs(oy - ay) < ry2;
       const bool rg = abs(ox - gx) < rx && 2 * abs(oy - gy) < ry2;
       if (!ra && !rg) break;
       if (++guard > REJECT_LIMIT) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
     }
-    p.st.static_obs[(int64_t)k * N + i] = pk(ox, oy);
+    p.static_obs[(int64_t)k * N + i] = pk(ox, oy);
     int f, e;
     if (g.near(ox, oy, f, e)) nl.push(f, e);
   }
-  for (int k = 0; k < c.num_dynamic; ++k) {                             // :153-164
-    const int ox = ds.draw(c.strip_obs_x, W - c.strip_obs_x);
-    const int oy = ds.draw(c.strip_obs_y, H - c.strip_obs_y);
-    p.st.dyn_obs[(int64_t)k * N + i] = pk(ox, oy);
-    p.st.dyn_goal[(int64_t)k * N + i] = (uint8_t)k;                    // curr_goal = goal list[k]
+  for (int k = 0; k < p.nd; ++k) {                                      // :153-164
+    const int ox = ds.draw(t.strip_obs_x, W - t.strip_obs_x);
+    const int oy = ds.draw(t.strip_obs_y, H - t.strip_obs_y);
+    p.dyn_obs[(int64_t)k * N + i] = pk(ox, oy);
+    p.dyn_goal[(int64_t)k * N + i] = (uint8_t)k;                       // curr_goal = goal list[k]
+    int f, e;
+    if (g.near(ox, oy, f, e)) nl.push(f, e);
+  }
+}
+
+// Perf-mode (Philox) reset, split over the env's LPE lanes.  Each quantity has its
+// own counter, so the lanes draw in parallel and nothing is serial but the
+// (rare) agent re-sample loop:
+//   sub = 0                         words gx, gy, ax, ay
+//   sub = 1 + r                     agent re-sample r: words ax, ay
+//   sub = 1<<22 | k<<12 | a         static obstacle k, attempt a: words x, y
+//   sub = 2<<22 | k<<12             dynamic obstacle k: words x, y
+// Distributions and rejection rules are the reference's (ballenv_env.py:113-167);
+// only the order in which the random words are consumed differs from numpy's
+// single stream, which the tape mode (reset_env) reproduces exactly.
+template <int BLOCK, int LPE>
+__device__ void reset_env_philox(const KParams& p, const Tables& t, int i, int q, uint32_t gid, uint32_t episode,
+                                 int& ax, int& ay, int& gx, int& gy, NearList<BLOCK>& nl) {
+  const int N = p.n, W = p.screen_w, H = p.screen_h;
+  const u4 b0 = philox(gid, episode, 0u, tag(PURPOSE_RESET, 0), p.seed);
+  gx = map_range(b0.x, W - t.strip_goal_x, W);
+  gy = map_range(b0.y, H - t.strip_goal_y, H);
+  ax = map_range(b0.z, 0, t.strip_agent_x);
+  ay = map_range(b0.w, 0, t.strip_agent_y);
+  const double dist = calc_dist(gx, gy, ax, ay);
+  for (int r = 0; calc_dist(gx, gy, ax, ay) < p.min_spawn_dist; ++r) {
+    if (r >= REJECT_LIMIT - 1) { if (q == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+    const u4 b = philox(gid, episode, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
+    ax = map_range(b.x, 0, t.strip_agent_x);
+    ay = map_range(b.y, 0, t.strip_agent_y);
+  }
+  if (q == 0) {
+    p.agent[i] = pk(ax, ay);
+    p.goal[i] = pk(gx, gy);
+    p.prev_dist[i] = dist;  // pre-resample distance (Q9)
+    p.total_dist[i] = calc_dist(ax, ay, gx, gy);
+    p.ep_return[i] = 0.0;
+    p.ep_len[i] = 0;
+    p.episode[i] = episode;
+  }
+  const Win g(p, ax, ay);
+  nl.cnt = 0;
+  const int rx = t.radius_obstacle + t.radius_agent, ry2 = t.radius_obstacle + 2 * t.radius_agent;
+  for (int k = q; k < p.ns; k += LPE) {
+    int ox = 0, oy = 0;
+    for (int a = 0;; ++a) {
+      const u4 b = philox(gid, episode, 0u, tag(PURPOSE_RESET, (1u << 22) | ((uint32_t)k << 12) | (uint32_t)a), p.seed);
+      ox = map_range(b.x, t.strip_obs_x, W - t.strip_obs_x);
+      oy = map_range(b.y, t.strip_obs_y, H - t.strip_obs_y);
+      const bool ra = abs(ox - ax) < rx && 2 * abs(oy - ay) < ry2;
+      const bool rg = abs(ox - gx) < rx && 2 * abs(oy - gy) < ry2;
+      if (!ra && !rg) break;
+      if (a >= REJECT_LIMIT - 1) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+    }
+    p.static_obs[(int64_t)k * N + i] = pk(ox, oy);
+    int f, e;
+    if (g.near(ox, oy, f, e)) nl.push(f, e);
+  }
+  for (int k = q; k < p.nd; k += LPE) {
+    const u4 b = philox(gid, episode, 0u, tag(PURPOSE_RESET, (2u << 22) | ((uint32_t)k << 12)), p.seed);
+    const int ox = map_range(b.x, t.strip_obs_x, W - t.strip_obs_x);
+    const int oy = map_range(b.y, t.strip_obs_y, H - t.strip_obs_y);
+    p.dyn_obs[(int64_t)k * N + i] = pk(ox, oy);
+    p.dyn_goal[(int64_t)k * N + i] = (uint8_t)k;
     int f, e;
     if (g.near(ox, oy, f, e)) nl.push(f, e);
   }
 }
 
 // ------------------------------------------------------------------ statistics
-__device__ __forceinline__ void atomic_min_f64(double* a, double v) {
-  unsigned long long* u = reinterpret_cast<unsigned long long*>(a);
-  unsigned long long old = *u;
-  while (v < __longlong_as_double((long long)old)) {
-    unsigned long long prev = atomicCAS(u, old, (unsigned long long)__double_as_longlong(v));
-    if (prev == old) break;
-    old = prev;
-  }
-}
-__device__ __forceinline__ void atomic_max_f64(double* a, double v) {
-  unsigned long long* u = reinterpret_cast<unsigned long long*>(a);
-  unsigned long long old = *u;
-  while (v > __longlong_as_double((long long)old)) {
-    unsigned long long prev = atomicCAS(u, old, (unsigned long long)__double_as_longlong(v));
-    if (prev == old) break;
-    old = prev;
-  }
-}
+// Finished-episode statistics go to per-block slots (slots, 8) f64:
+// [count, sum return, sum return^2, sum length, min return, max return, 0, 0].
+// A block's thread 0 read-modify-writes only its own slot, so there are no
+// atomics and no contention; be_stats_slots() tells the caller how many slots.
+struct WaveStats { double n, s1, s2, sl, mn, mx; };
 
-// Wave-level reduction of finished-episode statistics (called by all 64 lanes).
-__device__ void wave_stats(double* stats, bool done, double ret, int len) {
+__device__ __forceinline__ WaveStats wave_stats(bool done, double ret, int len) {
+  WaveStats w{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   const unsigned long long m = __ballot(done);
-  if (m == 0ull) return;  // wave-uniform: nobody finished (the common case)
+  if (m == 0ull) return w;  // wave-uniform: nobody finished (the common case)
   double s1 = done ? ret : 0.0, s2 = done ? ret * ret : 0.0, sl = done ? (double)len : 0.0;
   double mn = done ? ret : INFINITY, mx = done ? ret : -INFINITY;
 #pragma unroll
@@ -388,253 +485,402 @@ __device__ void wave_stats(double* stats, bool done, double ret, int len) {
     s1 += __shfl_xor(s1, o); s2 += __shfl_xor(s2, o); sl += __shfl_xor(sl, o);
     mn = fmin(mn, __shfl_xor(mn, o)); mx = fmax(mx, __shfl_xor(mx, o));
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&stats[0], (double)__popcll(m));
-    atomicAdd(&stats[1], s1); atomicAdd(&stats[2], s2); atomicAdd(&stats[3], sl);
-    atomic_min_f64(&stats[4], mn); atomic_max_f64(&stats[5], mx);
-  }
+  w.n = (double)__popcll(m); w.s1 = s1; w.s2 = s2; w.sl = sl; w.mn = mn; w.mx = mx;
+  return w;
 }
 
-constexpr int block_for(int WT) {
-  return WT == 0 ? 64 : ((4 + WT * WT) <= 256 ? 256 : ((4 + WT * WT) <= 512 ? 128 : 64));
+// ------------------------------------------------------------------ lane groups
+// LPE lanes cooperate on one env: obstacle k belongs to lane k % LPE, obs word w to lane w % LPE.
+constexpr int BLOCK_THREADS = 256;
+template <int LPE>
+__device__ __forceinline__ uint32_t group_or(uint32_t x) {
+  static_assert(LPE == 1 || LPE == 2 || LPE == 4, "LPE must be 1, 2 or 4");
+  if constexpr (LPE >= 2) x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+  if constexpr (LPE >= 4) x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+  return x;
+}
+template <int LPE>
+__device__ __forceinline__ int group_bcast(int x) {  // value of the group's lane 0
+  if constexpr (LPE == 1) return x;
+  else if constexpr (LPE == 2) return __builtin_amdgcn_update_dpp(0, x, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
+  else return __builtin_amdgcn_update_dpp(0, x, 0x00, 0xF, 0xF, false);                          // quad_perm 0,0,0,0
 }
 
-// One dynamic obstacle's move_obstacles (ballenv_env.py:323-353).  d0/d1 are
-// the values of its first/second randint call (tape or Philox mapped below).
-struct DynMove {
-  __device__ static void apply(const KArgs& p, int64_t a, int& ox, int& oy, int gi, int speed, bool change,
-                               bool tape, int t0, int t1, uint32_t w0, uint32_t w1) {
-    const be_config& c = p.c;
-    if (!change) {
-      const int32_t gp = p.t.goal[gi];
-      const int tx = px(gp) - ox, ty = py(gp) - oy;
-      int mv;  // -1 = directed move toward the current goal
-      if (tx != 0 && ty != 0) {
-        const int u = tape ? t0 : map_range(w0, 0, 100);
-        mv = u < c.obs_certainty ? -1 : (tape ? t1 : map_range(w1, 0, 9));
-      } else {
-        mv = tape ? t0 : map_range(w0, 0, 9);
-      }
-      int mx, my;
-      if (mv < 0) { mx = tx > 0 ? 1 : -1; my = ty > 0 ? 1 : -1; }
-      else {  // move_list of ballenv_env.py:324: (-1,-1) twice, no (-1,0) (Q4)
-        mx = mv < 3 ? 1 : (mv < 6 ? 0 : -1);
-        const int r3 = mv - 3 * (mv / 3);
-        my = mv == 8 ? -1 : (r3 == 0 ? 1 : (r3 == 1 ? -1 : 0));
-      }
-      ox += mx * speed; oy += my * speed;
-      if (ox < -32768 || ox > 32767 || oy < -32768 || oy > 32767) atomicOr(p.status, BE_STATUS_COORD_RANGE);
-      p.st.dyn_obs[a] = pk(ox, oy);
-    } else {  // new goal from the other goals; no move this step (Q5)
-      const int n_other = p.t.n_other[gi];
-      if (n_other == 0) atomicOr(p.status, BE_STATUS_NO_GOAL);
-      else p.st.dyn_goal[a] = p.t.other[gi][tape ? t0 : map_range(w0, 0, n_other)];
+constexpr int lanes_for(int WT) { return WT == 0 ? 1 : 4; }
+constexpr int envs_per_block(int WT) { return BLOCK_THREADS / lanes_for(WT); }
+
+// One dynamic obstacle's move_obstacles (ballenv_env.py:323-353).  Tape mode: t0/t1
+// are the values of its first/second randint call.  Philox mode: both draws come
+// from one 32-bit word w -- randint(n0) = hi32(w*n0), then randint(n1) =
+// hi32(lo32(w*n0)*n1) (the multiply-shift's fractional part).
+__device__ __forceinline__ void dyn_move(const KParams& p, const Tables& t, int64_t a, int& ox, int& oy, int gi,
+                                         int speed, bool change, bool tape, int t0, int t1, uint32_t w) {
+  if (!change) {
+    const int32_t gp = t.goal[gi];
+    const int tx = px(gp) - ox, ty = py(gp) - oy;
+    int mv;  // -1 = directed move toward the current goal
+    if (tx != 0 && ty != 0) {
+      const int u = tape ? t0 : (int)__umulhi(w, 100u);
+      mv = u < p.certainty ? -1 : (tape ? t1 : (int)__umulhi(w * 100u, 9u));
+    } else {
+      mv = tape ? t0 : (int)__umulhi(w, 9u);
     }
+    int mx, my;
+    if (mv < 0) { mx = tx > 0 ? 1 : -1; my = ty > 0 ? 1 : -1; }
+    else {  // move_list of ballenv_env.py:324: (-1,-1) twice, no (-1,0) (Q4)
+      mx = mv < 3 ? 1 : (mv < 6 ? 0 : -1);
+      const int r3 = mv - 3 * (mv / 3);
+      my = mv == 8 ? -1 : (r3 == 0 ? 1 : (r3 == 1 ? -1 : 0));
+    }
+    ox += mx * speed; oy += my * speed;
+    if (ox < -32768 || ox > 32767 || oy < -32768 || oy > 32767) atomicOr(p.status, BE_STATUS_COORD_RANGE);
+    p.dyn_obs[a] = pk(ox, oy);
+  } else {  // new goal from the other goals; no move this step (Q5)
+    const int n_other = t.n_other[gi];
+    if (n_other == 0) atomicOr(p.status, BE_STATUS_NO_GOAL);
+    else p.dyn_goal[a] = t.other[gi][tape ? t0 : (int)__umulhi(w, (uint32_t)n_other)];
   }
-};
+}
 
 // ------------------------------------------------------------------ the kernel
 // MODE_STEP: physics + (autoreset) + obs.  MODE_RESET: reset masked envs + obs.
 // MODE_OBSERVE: obs only.  WT = compile-time W (0 = runtime W, no LDS staging).
+// LPE = lanes per env (4 for compiled W): at 65536 envs that is 4 waves per SIMD
+// instead of 1, so the waves hide each other's memory and ALU latency.
 template <int WT, int MODE>
-__global__ __launch_bounds__(block_for(WT)) void be_kernel(KArgs p) {
-  constexpr int BLOCK = block_for(WT);
+__global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
+  constexpr int LPE = lanes_for(WT);
+  constexpr int EPB = envs_per_block(WT);
+  constexpr int SPL = CS / LPE, DPL = CD / LPE;   // obstacle slots per lane in the register chunk
   extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Tables t;
+  __shared__ WaveStats s_ws[BLOCK_THREADS / 64];
+  constexpr int TW = (int)(sizeof(Tables) / 4);
+  static_assert(TW <= BLOCK_THREADS && sizeof(Tables) % 4 == 0, "table staging assumes <= 256 words");
 
-  const be_config& c = p.c;
-  const int N = c.num_envs, Ns = c.num_static, Nd = c.num_dynamic;
+  DIAG(0);
+  if (p.dbg & DBG_EXIT_ENTRY) return;
+  const int N = p.n, Ns = p.ns, Nd = p.nd;
   const int tid = threadIdx.x;
-  const int i = blockIdx.x * BLOCK + tid;
+  const int q = tid & (LPE - 1);                  // lane within the env's group
+  const int el = tid / LPE;                        // env within the block
+  const int i = blockIdx.x * EPB + el;
   const bool valid = i < N;
+  const bool lead = q == 0;                        // the group lane that owns per-env stores
 
-  NearList<BLOCK> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
+  // LDS: [near lists: nobs slots x 256 lanes x 4 B][obs stage: EPB x F bytes]
+  NearList<BLOCK_THREADS> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
+  uint8_t* stage = smem + (size_t)(Ns + Nd) * BLOCK_THREADS * 4;
+
   int ax = 0, ay = 0, gx = 0, gy = 0;
   bool done = false;
   double fin_ret = 0.0;
   int fin_len = 0;
   uint32_t episode = 0;
-  const uint32_t gid = (uint32_t)(c.env_offset + i);
+  const uint32_t gid = (uint32_t)p.gid0 + (uint32_t)i;
 
+  // ---- phase 0: issue every load of this env (independent, coalesced across the wave)
+  //      together with the block's table words; one barrier then covers them all.
+  int a = 0, dx = 0, dy = 0, len0 = 0;
+  int32_t agent0 = 0, goal0 = 0;
+  double old_dist = 0.0, total = 1.0, ret = 0.0;
+  const int ns0 = min(Ns, CS), nd0 = min(Nd, CD);
+  int32_t so[SPL], dp[DPL];
+  int dgi[DPL], t0[DPL], t1[DPL];
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) so[j] = 0;
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) { dp[j] = 0; dgi[j] = 0; t0[j] = 0; t1[j] = 0; }
+  const uint32_t tword = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
   if (valid) {
+    agent0 = p.agent[i];
+    goal0 = p.goal[i];
     if (MODE == MODE_STEP) {
-      // ---- issue every load of this env first (independent, coalesced across the wave)
-      int a = 0, dx = 0, dy = 0;
       if (p.actions) a = p.actions[i];
       else if (p.deltas) { dx = p.deltas[2 * (int64_t)i]; dy = p.deltas[2 * (int64_t)i + 1]; }
-      const int32_t agent0 = p.st.agent[i];
-      const int32_t goal0 = p.st.goal[i];
-      const double old_dist = p.st.prev_dist[i];
-      const double total = p.st.total_dist[i];
-      double ret = p.st.ep_return[i];
-      const int len0 = p.st.ep_len[i];
-      episode = p.st.episode[i];
-      const int ns0 = min(Ns, CS), nd0 = min(Nd, CD);
-      int32_t so[CS], dp[CD];
-      int dgi[CD], t0[CD], t1[CD];
+      old_dist = p.prev_dist[i];
+      total = p.total_dist[i];
+      ret = p.ep_return[i];
+      len0 = p.ep_len[i];
 #pragma unroll
-      for (int k = 0; k < CS; ++k) so[k] = k < ns0 ? p.st.static_obs[(int64_t)k * N + i] : 0;
-#pragma unroll
-      for (int k = 0; k < CD; ++k) {
-        dp[k] = k < nd0 ? p.st.dyn_obs[(int64_t)k * N + i] : 0;
-        dgi[k] = k < nd0 ? p.st.dyn_goal[(int64_t)k * N + i] : 0;
-        t0[k] = (p.tape && k < nd0) ? p.tape[(int64_t)(2 * k) * N + i] : 0;
-        t1[k] = (p.tape && k < nd0) ? p.tape[(int64_t)(2 * k + 1) * N + i] : 0;
+      for (int j = 0; j < SPL; ++j) {
+        const int k = q + LPE * j;
+        if (k < ns0) so[j] = p.static_obs[(int64_t)k * N + i];
       }
-
-      // ---- action -> agent move + clamp (ballenv_env.py:247-259)
-      if (p.actions) {
-        if (a >= c.num_actions) { atomicOr(p.status, BE_STATUS_BAD_ACTION); a = 0; }
-        const int32_t m = p.t.action[a]; dx = px(m); dy = py(m);
-      } else if (!p.deltas) {  // sampled actions
-        const u4 b = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_ACTION, 0), c.seed);
-        const int32_t m = p.t.action[map_range(b.x, 0, c.num_actions)]; dx = px(m); dy = py(m);
-      }
-      gx = px(goal0); gy = py(goal0);
-      ax = min(max(px(agent0) + c.speed_x * dx, 0), c.screen_width);
-      ay = min(max(py(agent0) + c.speed_y * dy, 0), c.screen_height);
-      const Win g(c, ax, ay);
-      const uint32_t R2 = (uint32_t)g.R2;
-      bool hs = false, hd = false;
-
-      // ---- dynamic obstacles: move (counter == ep_len mod (G+1): all start at 0 on reset)
-      const int counter = len0 % (c.goal_change_step + 1);
-      const bool change = counter >= c.goal_change_step;
-      const bool tape = p.tape != nullptr;
-      u4 blk{0, 0, 0, 0};
 #pragma unroll
-      for (int k = 0; k < CD; ++k) {
+      for (int j = 0; j < DPL; ++j) {
+        const int k = q + LPE * j;
         if (k < nd0) {
-          // Philox block k>>1 holds both draws of obstacles 2j and 2j+1
-          if (!tape && (k & 1) == 0) blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, k >> 1), c.seed);
-          int ox = px(dp[k]), oy = py(dp[k]);
-          DynMove::apply(p, (int64_t)k * N + i, ox, oy, dgi[k], c.obstacle_speed[k], change, tape, t0[k], t1[k],
-                         (k & 1) ? blk.z : blk.x, (k & 1) ? blk.w : blk.y);
-          hd |= d2u(ox - ax, oy - ay) <= R2;
-          int f, e;
-          if (g.near(ox, oy, f, e)) nl.push(f, e);
+          dp[j] = p.dyn_obs[(int64_t)k * N + i];
+          dgi[j] = p.dyn_goal[(int64_t)k * N + i];
+          if (p.tape) { t0[j] = p.tape[(int64_t)(2 * k) * N + i]; t1[j] = p.tape[(int64_t)(2 * k + 1) * N + i]; }
         }
       }
-      for (int kb = CD; kb < Nd; ++kb) {  // configs with more than CD dynamic obstacles
+    }
+    if (MODE != MODE_OBSERVE) episode = p.episode[i];
+  }
+  if (tid < TW) reinterpret_cast<uint32_t*>(&t)[tid] = tword;
+  __syncthreads();  // the block's first barrier: tables staged, all loads above have landed
+  DIAG(1);
+  if (p.dbg & DBG_EXIT_BARRIER) {
+    if (valid && (agent0 ^ goal0 ^ so[0] ^ dp[0] ^ (int)len0 ^ (int)old_dist) == 0x7fffffff) p.obs[i] = 1;
+    return;
+  }
+
+  if (valid) {
+    gx = px(goal0); gy = py(goal0);
+    if (MODE == MODE_STEP) {
+      // ---- action -> agent move + clamp (ballenv_env.py:247-259); every lane of the group
+      if (p.actions) {
+        if (a >= p.num_actions) { if (lead) atomicOr(p.status, BE_STATUS_BAD_ACTION); a = 0; }
+        const int32_t m = t.action[a]; dx = px(m); dy = py(m);
+      } else if (!p.deltas) {  // sampled actions
+        const u4 b = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_ACTION, 0), p.seed);
+        const int32_t m = t.action[map_range(b.x, 0, p.num_actions)]; dx = px(m); dy = py(m);
+      }
+      ax = min(max(px(agent0) + p.speed_x * dx, 0), p.screen_w);
+      ay = min(max(py(agent0) + p.speed_y * dy, 0), p.screen_h);
+      const Win g(p, ax, ay);
+      const uint32_t R2 = (uint32_t)g.R2;
+      bool hs = false, hd = false;
+      DIAG(8);
+
+      // ---- dynamic obstacles: move (counter == ep_len mod (G+1): all start at 0 on reset)
+      int counter = (int)((double)len0 * p.inv_g1);
+      counter = len0 - counter * (p.goal_change + 1);
+      if (counter < 0) counter += p.goal_change + 1;
+      if (counter > p.goal_change) counter -= p.goal_change + 1;
+      const bool change = counter >= p.goal_change;
+      const bool tape = p.tape != nullptr;
+      // Philox words: obstacle k uses word k&3 of block k>>2.  With 4 lanes per env every
+      // lane computes ONE block (block = lane parity) and the pair swaps words by DPP.
+      uint32_t wj[DPL];
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) wj[j] = 0u;
+      if (!tape && !(p.dbg & DBG_NO_PHILOX)) {
+        if constexpr (LPE == 4) {
+          const u4 blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(q & 1)), p.seed);
+          const uint32_t own = pick_word(blk, q), send = pick_word(blk, q ^ 1);
+          const uint32_t recv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xF, 0xF, false);
+          wj[0] = (q & 1) ? recv : own;   // k = q     : block 0, word q
+          wj[1] = (q & 1) ? own : recv;   // k = q + 4 : block 1, word q
+        } else {
+          u4 blk{0, 0, 0, 0};
+#pragma unroll
+          for (int j = 0; j < DPL; ++j) {
+            const int k = q + LPE * j;
+            if (((k & 3) == 0 || j == 0) && k < nd0) blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(k >> 2)), p.seed);
+            wj[j] = pick_word(blk, k & 3);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) {
+        const int k = q + LPE * j;
+        if (k < nd0) {
+          int ox = px(dp[j]), oy = py(dp[j]);
+          if (!(p.dbg & DBG_NO_DYN))
+            dyn_move(p, t, (int64_t)k * N + i, ox, oy, dgi[j], t.speed[k], change, tape, t0[j], t1[j], wj[j]);
+          hd |= d2u(ox - ax, oy - ay) <= R2;
+          int f, e;
+          if (g.near(ox, oy, f, e) && !(p.dbg & DBG_NO_NEAR)) nl.push(f, e);
+        }
+      }
+      for (int kb = CD + q; kb < Nd; kb += LPE) {  // configs with more than CD dynamic obstacles
         const int64_t aa = (int64_t)kb * N + i;
-        int ox = px(p.st.dyn_obs[aa]), oy = py(p.st.dyn_obs[aa]);
-        if (!tape && (kb & 1) == 0) blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, kb >> 1), c.seed);
+        int ox = px(p.dyn_obs[aa]), oy = py(p.dyn_obs[aa]);
+        const u4 blk = tape ? u4{0, 0, 0, 0} : philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(kb >> 2)), p.seed);
         const int tt0 = tape ? p.tape[(int64_t)(2 * kb) * N + i] : 0, tt1 = tape ? p.tape[(int64_t)(2 * kb + 1) * N + i] : 0;
-        DynMove::apply(p, aa, ox, oy, p.st.dyn_goal[aa], c.obstacle_speed[kb], change, tape, tt0, tt1,
-                       (kb & 1) ? blk.z : blk.x, (kb & 1) ? blk.w : blk.y);
+        dyn_move(p, t, aa, ox, oy, p.dyn_goal[aa], t.speed[kb], change, tape, tt0, tt1, pick_word(blk, kb & 3));
         hd |= d2u(ox - ax, oy - ay) <= R2;
         int f, e;
         if (g.near(ox, oy, f, e)) nl.push(f, e);
       }
+      DIAG(9);
       // ---- static obstacles: collision + near test
 #pragma unroll
-      for (int k = 0; k < CS; ++k) {
+      for (int j = 0; j < SPL; ++j) {
+        const int k = q + LPE * j;
         if (k < ns0) {
-          const int ox = px(so[k]), oy = py(so[k]);
+          const int ox = px(so[j]), oy = py(so[j]);
           hs |= d2u(ox - ax, oy - ay) <= R2;
           int f, e;
-          if (g.near(ox, oy, f, e)) nl.push(f, e);
+          if (g.near(ox, oy, f, e) && !(p.dbg & DBG_NO_NEAR)) nl.push(f, e);
         }
       }
-      for (int kb = CS; kb < Ns; ++kb) {
-        const int32_t o = p.st.static_obs[(int64_t)kb * N + i];
+      for (int kb = CS + q; kb < Ns; kb += LPE) {
+        const int32_t o = p.static_obs[(int64_t)kb * N + i];
         const int ox = px(o), oy = py(o);
         hs |= d2u(ox - ax, oy - ay) <= R2;
         int f, e;
         if (g.near(ox, oy, f, e)) nl.push(f, e);
       }
+      // the group's collision flags (every lane of a valid group is active here)
+      hs = group_or<LPE>((uint32_t)hs) != 0u;
+      hd = group_or<LPE>((uint32_t)hd) != 0u;
 
+      DIAG(10);
       // ---- distance, reward, done (ballenv_env.py:268-286, 200-229)
       const double dist = calc_dist(gx, gy, ax, ay);
-      double reward = 0.0 - c.time_penalty;
+      double reward = 0.0 - p.time_penalty;
       reward += (old_dist - dist) / total;
-      if (hs) reward -= c.static_penalty;          // statics come first in obstacle_list (Q3)
-      else if (hd) reward -= c.dynamic_penalty;
+      if (hs) reward -= p.static_penalty;          // statics come first in obstacle_list (Q3)
+      else if (hd) reward -= p.dynamic_penalty;
       ret += reward;
       const int len = len0 + 1;
-      const bool env_done = (dist < c.threshold_goal) || hs || hd;
-      const bool trunc = c.time_limit > 0 && len >= c.time_limit;
+      const bool env_done = (dist < p.threshold_goal) || hs || hd;
+      const bool trunc = p.time_limit > 0 && len >= p.time_limit;
       done = env_done || trunc;
-      p.out.reward[i] = reward;
-      p.out.done[i] = (uint8_t)done;
-      if (p.out.truncated) p.out.truncated[i] = (uint8_t)(trunc && !env_done);
-      p.st.agent[i] = pk(ax, ay);
-      p.st.prev_dist[i] = dist;
-      p.st.ep_return[i] = ret;
-      p.st.ep_len[i] = len;
-      if (done) {
-        if (p.out.final_return) p.out.final_return[i] = ret;
-        if (p.out.final_len) p.out.final_len[i] = len;
+      if (lead) {
+        p.reward[i] = reward;
+        p.done[i] = (uint8_t)done;
+        if (p.truncated) p.truncated[i] = (uint8_t)(trunc && !env_done);
+        p.agent[i] = pk(ax, ay);
+        p.prev_dist[i] = dist;
+        p.ep_return[i] = ret;
+        p.ep_len[i] = len;
+        if (done) {
+          if (p.final_return) p.final_return[i] = ret;
+          if (p.final_len) p.final_len[i] = len;
+        }
       }
       fin_ret = ret; fin_len = len;
     } else {
-      const int32_t agent0 = p.st.agent[i];
-      const int32_t goal0 = p.st.goal[i];
-      ax = px(agent0); ay = py(agent0); gx = px(goal0); gy = py(goal0);
-      if (MODE == MODE_RESET) episode = p.st.episode[i];
+      ax = px(agent0); ay = py(agent0);
     }
   }
-  if (MODE == MODE_STEP && p.out.stats) wave_stats(p.out.stats, done, fin_ret, fin_len);  // all lanes converged
+  DIAG(2);
+  if (p.dbg & DBG_EXIT_PHYSICS) return;
+  WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
+  if (MODE == MODE_STEP && p.stats && !(p.dbg & DBG_NO_STATS))
+    ws = wave_stats(done && lead, fin_ret, fin_len);  // all lanes converged here
 
-  // ---- episode boundary: terminal obs + reset (rare, divergent)
+  // ---- episode boundary: terminal obs + reset (rare; the whole group takes the branch)
   bool do_reset = false;
   if (valid) {
-    if (MODE == MODE_STEP) do_reset = done && c.autoreset;
+    if (MODE == MODE_STEP) do_reset = done && p.autoreset;
     if (MODE == MODE_RESET) do_reset = p.mask ? (p.mask[i] != 0) : true;
   }
   if (valid && do_reset) {
-    if (MODE == MODE_STEP && p.out.terminal_obs) {
-      const int F = 4 + c.window * c.window;
-      const Win g(c, ax, ay);
+    if (MODE == MODE_STEP && p.terminal_obs) {
+      const int F = 4 + p.window * p.window;
+      const Win g(p, ax, ay);
       const int quad = quadrant(ax, ay, gx, gy);
       if constexpr (WT > 0) {
         uint32_t rows[Geo<WT>::K], flat[Geo<WT>::NW];
-        raster_rows<WT, BLOCK>(nl, g, rows);
+        raster_rows<WT, BLOCK_THREADS>(nl, g, rows);
+#pragma unroll
+        for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k]);
         flatten<WT>(rows, flat);
-        write_row_global<WT>(p.out.terminal_obs + (int64_t)i * F, flat, quad);
+        if (lead) write_row_global<WT>(p.terminal_obs + (int64_t)i * F, flat, quad);
       } else {
-        write_row_generic<BLOCK>(nl, g, quad, p.out.terminal_obs + (int64_t)i * F, nullptr);
+        write_row_generic<BLOCK_THREADS>(nl, g, quad, p.terminal_obs + (int64_t)i * F, nullptr);
       }
     }
-    ResetDraws ds{MODE == MODE_RESET ? p.reset_tape : nullptr, p.reset_tape_len, N, i, 0, gid, episode + 1u,
-                  c.seed, p.status};
-    reset_env<BLOCK>(p, i, ds, ax, ay, gx, gy, nl);
+    if (MODE == MODE_RESET && p.reset_tape) {
+      // parity mode: the reference's single sequential draw stream, on the lead lane
+      if (lead) {
+        ResetDraws ds{p.reset_tape, p.reset_tape_len, N, i, 0, gid, episode + 1u, p.seed, p.status};
+        reset_env<BLOCK_THREADS>(p, t, i, ds, ax, ay, gx, gy, nl);   // lead lane's list gets every obstacle
+      } else {
+        nl.cnt = 0;
+      }
+      ax = group_bcast<LPE>(ax); ay = group_bcast<LPE>(ay);
+      gx = group_bcast<LPE>(gx); gy = group_bcast<LPE>(gy);
+    } else {
+      reset_env_philox<BLOCK_THREADS, LPE>(p, t, i, q, gid, episode + 1u, ax, ay, gx, gy, nl);
+    }
   } else if (valid && MODE != MODE_STEP) {
-    // observe / reset of an unmasked env: near list of the current state
-    const Win g(c, ax, ay);
-    for (int k = 0; k < Ns; ++k) {
-      const int32_t o = p.st.static_obs[(int64_t)k * N + i];
+    // observe / reset of an unmasked env: near list of the current state, split over the group
+    const Win g(p, ax, ay);
+    for (int k = q; k < Ns; k += LPE) {
+      const int32_t o = p.static_obs[(int64_t)k * N + i];
       int f, e;
       if (g.near(px(o), py(o), f, e)) nl.push(f, e);
     }
-    for (int k = 0; k < Nd; ++k) {
-      const int32_t o = p.st.dyn_obs[(int64_t)k * N + i];
+    for (int k = q; k < Nd; k += LPE) {
+      const int32_t o = p.dyn_obs[(int64_t)k * N + i];
       int f, e;
       if (g.near(px(o), py(o), f, e)) nl.push(f, e);
     }
   }
 
+  DIAG(3);
   // ---- observation (prep_state4)
   if constexpr (WT > 0) {
+    constexpr int F = Geo<WT>::F;
     uint32_t flat[Geo<WT>::NW];
     int quad = 0;
     if (valid) {
-      const Win g(c, ax, ay);
+      const Win g(p, ax, ay);
       uint32_t rows[Geo<WT>::K];
-      raster_rows<WT, BLOCK>(nl, g, rows);
+      if (p.dbg & DBG_NO_RASTER) nl.cnt = 0;
+      raster_rows<WT, BLOCK_THREADS>(nl, g, rows);
+#pragma unroll
+      for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k]);
       flatten<WT>(rows, flat);
       quad = quadrant(ax, ay, gx, gy);
     }
-    __syncthreads();  // near lists consumed: the stage reuses the same LDS
-    if (valid) stage_row<WT>(smem, tid, flat, quad);
-    __syncthreads();
-    const int nvalid = min(BLOCK, N - (int)blockIdx.x * BLOCK);
-    copy_out<BLOCK>(smem, Geo<WT>::F, nvalid, (int64_t)blockIdx.x * BLOCK, p.out.obs, p.out.obs_f32);
+    if (p.dbg & (DBG_NO_OBS | DBG_EXIT_RASTER)) {
+      if (valid && flat[0] == 0x12345u && quad == 7) p.obs[i] = 1;   // keep the rows live
+      return;
+    }
+    if (valid) {  // lane q writes words (bytes, when F % 4 != 0) q, q+LPE, ... of its env's row
+      if constexpr ((F & 3) == 0) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(stage + el * F);
+#pragma unroll
+        for (int w0 = 0; w0 < F / 4; w0 += LPE) {
+          const int w = w0 + q;
+          if (w < F / 4) {
+            uint32_t v;
+            if (w == 0) v = 1u << (8 * quad);
+            else {
+              const int jc = 4 * (w - 1);  // first cell of this word (nibble aligned)
+              const uint32_t nib = (flat[jc >> 5] >> (jc & 31)) & 0xFu;
+              v = (nib * 0x00204081u) & 0x01010101u;
+            }
+            dst[w] = v;
+          }
+        }
+      } else {
+        uint8_t* dst = stage + el * F;
+#pragma unroll
+        for (int b0 = 0; b0 < F; b0 += LPE) {
+          const int b = b0 + q;
+          if (b < F) dst[b] = (uint8_t)obs_byte<WT>(flat, quad, b);
+        }
+      }
+    }
+    if (MODE == MODE_STEP && (tid & 63) == 0) s_ws[tid >> 6] = ws;
+    DIAG(4);
+    __syncthreads();  // stage complete
+    DIAG(5);
+    const int nvalid = min(EPB, N - (int)blockIdx.x * EPB);
+    copy_out<BLOCK_THREADS>(stage, F, nvalid, (int64_t)blockIdx.x * EPB, p.obs, p.obs_f32);
   } else {
-    if (valid) {
-      const int F = 4 + c.window * c.window;
-      const Win g(c, ax, ay);
-      write_row_generic<BLOCK>(nl, g, quadrant(ax, ay, gx, gy), p.out.obs ? p.out.obs + (int64_t)i * F : nullptr,
-                               p.out.obs_f32 ? p.out.obs_f32 + (int64_t)i * F : nullptr);
+    if (valid && lead) {
+      const int F = 4 + p.window * p.window;
+      const Win g(p, ax, ay);
+      write_row_generic<BLOCK_THREADS>(nl, g, quadrant(ax, ay, gx, gy), p.obs ? p.obs + (int64_t)i * F : nullptr,
+                                       p.obs_f32 ? p.obs_f32 + (int64_t)i * F : nullptr);
+    }
+    if (MODE == MODE_STEP && (tid & 63) == 0) s_ws[tid >> 6] = ws;
+    __syncthreads();
+  }
+
+  DIAG(6);
+  // ---- the block's statistics slot (thread 0 only; no other block touches it)
+  if (MODE == MODE_STEP && p.stats && tid == 0) {
+    WaveStats b = s_ws[0];
+#pragma unroll
+    for (int w = 1; w < BLOCK_THREADS / 64; ++w) {
+      const WaveStats& o = s_ws[w];
+      b.n += o.n; b.s1 += o.s1; b.s2 += o.s2; b.sl += o.sl; b.mn = fmin(b.mn, o.mn); b.mx = fmax(b.mx, o.mx);
+    }
+    if (b.n > 0.0) {
+      double* slot = p.stats + (size_t)blockIdx.x * 8;
+      slot[0] += b.n; slot[1] += b.s1; slot[2] += b.s2; slot[3] += b.sl;
+      slot[4] = fmin(slot[4], b.mn); slot[5] = fmax(slot[5], b.mx);
     }
   }
 }
@@ -651,30 +897,30 @@ __global__ void sample_actions_kernel(uint8_t* out, int32_t n, int32_t steps, in
 }
 
 // ------------------------------------------------------------------ dispatch
-using KFn = void (*)(KArgs);
+using KFn = void (*)(KParams);
 template <int WT>
 KFn kernel_for(int mode) {
   return mode == MODE_STEP ? be_kernel<WT, MODE_STEP>
                            : (mode == MODE_RESET ? be_kernel<WT, MODE_RESET> : be_kernel<WT, MODE_OBSERVE>);
 }
 
-struct Launch { KFn fn; int block; int lds; };
+struct Launch { KFn fn; int epb; int lds; };
 
 Launch pick_kernel(const be_config& c, int mode) {
   const int W = c.window, F = 4 + W * W, nobs = c.num_static + c.num_dynamic;
   Launch L{nullptr, 0, 0};
   bool staged = true;
   switch (W) {
-#define BE_CASE(n) case n: L.fn = kernel_for<n>(mode); L.block = block_for(n); break;
+#define BE_CASE(n) case n: L.fn = kernel_for<n>(mode); L.epb = envs_per_block(n); break;
     BE_CASE(1) BE_CASE(2) BE_CASE(3) BE_CASE(4) BE_CASE(5) BE_CASE(6) BE_CASE(7) BE_CASE(8)
     BE_CASE(9) BE_CASE(10) BE_CASE(11) BE_CASE(12) BE_CASE(13) BE_CASE(14) BE_CASE(15) BE_CASE(16)
     BE_CASE(21)
 #undef BE_CASE
-    default: L.fn = kernel_for<0>(mode); L.block = block_for(0); staged = false; break;
+    default: L.fn = kernel_for<0>(mode); L.epb = envs_per_block(0); staged = false; break;
   }
-  const int near_bytes = nobs * L.block * 4;
-  const int stage_bytes = staged ? L.block * F : 0;
-  L.lds = ((near_bytes > stage_bytes ? near_bytes : stage_bytes) + 15) & ~15;
+  const int near_bytes = nobs * BLOCK_THREADS * 4;
+  const int stage_bytes = staged ? L.epb * F : 0;
+  L.lds = (near_bytes + stage_bytes + 15) & ~15;
   if (L.lds == 0) L.lds = 16;
   return L;
 }
@@ -685,8 +931,10 @@ Launch pick_kernel(const be_config& c, int mode) {
 struct be_ctx {
   be_config cfg;
   Tables tables;
+  KParams base;      // config-derived part of every launch's KParams
   int device;
   int* status;
+  Tables* d_tables;
   char err[512];
 };
 
@@ -707,6 +955,20 @@ static int fail(be_ctx* ctx, int code, const char* fmt, const char* detail) {
 extern "C" {
 
 int be_abi_version(void) { return BE_ABI_VERSION; }
+
+#ifdef BE_DIAG_STAMPS
+// diagnostics build only: copy the stamp tables out (rt, cy: DIAG_WAVES x DIAG_POINTS each)
+int be_diag_stamps(unsigned long long* rt, unsigned long long* cy) {
+  if (hipMemcpyFromSymbol(rt, HIP_SYMBOL(g_diag_rt), sizeof(g_diag_rt)) != hipSuccess) return BE_E_HIP;
+  if (hipMemcpyFromSymbol(cy, HIP_SYMBOL(g_diag_cy), sizeof(g_diag_cy)) != hipSuccess) return BE_E_HIP;
+  return BE_OK;
+}
+int be_diag_clear(void) {
+  static unsigned long long zero[DIAG_WAVES][DIAG_POINTS];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_rt), zero, sizeof(zero)) != hipSuccess) return BE_E_HIP;
+  return BE_OK;
+}
+#endif
 
 int be_config_default(be_config* c, int32_t num_envs, int32_t window) {
   if (!c) return fail(nullptr, BE_E_INVALID, "%s", "cfg is NULL");
@@ -784,6 +1046,12 @@ int64_t be_step_bytes(const be_config* c) {
 
 const char* be_last_error(const be_ctx* ctx) { return ctx ? ctx->err : g_err; }
 
+int64_t be_stats_slots(const be_config* c) {
+  if (!c || c->num_envs < 1 || c->window < 1) return 0;
+  const Launch L = pick_kernel(*c, MODE_STEP);
+  return ((int64_t)c->num_envs + L.epb - 1) / L.epb;
+}
+
 int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   if (!out) return fail(nullptr, BE_E_INVALID, "%s", "out is NULL");
   *out = nullptr;
@@ -793,8 +1061,25 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   if (!ctx) return fail(nullptr, BE_E_NOMEM, "%s", "out of host memory");
   ctx->cfg = *cfg;
   ctx->device = device;
+  KParams& b = ctx->base;
+  memset(&b, 0, sizeof b);
+  b.n = cfg->num_envs; b.window = cfg->window; b.ns = cfg->num_static; b.nd = cfg->num_dynamic;
+  b.R = cfg->radius_obstacle + cfg->radius_agent; b.speed_x = cfg->speed_x; b.speed_y = cfg->speed_y;
+  b.screen_w = cfg->screen_width; b.screen_h = cfg->screen_height; b.goal_change = cfg->goal_change_step;
+  b.certainty = cfg->obs_certainty; b.time_limit = cfg->time_limit; b.num_actions = cfg->num_actions;
+  b.autoreset = cfg->autoreset; b.gid0 = (int32_t)(uint32_t)cfg->env_offset;
+  b.threshold_goal = cfg->threshold_goal; b.time_penalty = cfg->time_penalty;
+  b.static_penalty = cfg->static_penalty; b.dynamic_penalty = cfg->dynamic_penalty;
+  b.min_spawn_dist = cfg->min_spawn_dist; b.seed = cfg->seed;
+  b.inv_g1 = 1.0 / ((double)cfg->goal_change_step + 1.0);
+  if (const char* d = getenv("BALLENV_DEBUG_SKIP")) b.dbg = (int32_t)strtoul(d, nullptr, 0);
   Tables& t = ctx->tables;
   memset(&t, 0, sizeof t);
+  for (int k = 0; k < cfg->num_dynamic; ++k) t.speed[k] = cfg->obstacle_speed[k];
+  t.strip_obs_x = cfg->strip_obs_x; t.strip_obs_y = cfg->strip_obs_y;
+  t.strip_goal_x = cfg->strip_goal_x; t.strip_goal_y = cfg->strip_goal_y;
+  t.strip_agent_x = cfg->strip_agent_x; t.strip_agent_y = cfg->strip_agent_y;
+  t.radius_obstacle = cfg->radius_obstacle; t.radius_agent = cfg->radius_agent;
   for (int g = 0; g < cfg->num_goals; ++g)
     t.goal[g] = (int32_t)(((uint32_t)cfg->goals[g][0] & 0xFFFFu) | ((uint32_t)cfg->goals[g][1] << 16));
   for (int a = 0; a < cfg->num_actions; ++a)
@@ -808,10 +1093,13 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipMalloc(&ctx->status, sizeof(int));
   if (e == hipSuccess) e = hipMemset(ctx->status, 0, sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&ctx->d_tables, sizeof(Tables));
+  if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, &ctx->tables, sizeof(Tables), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     int rc = fail(nullptr, BE_E_HIP, "HIP error in be_create: %s", hipGetErrorString(e));
     if (ctx->status) (void)hipFree(ctx->status);
+    if (ctx->d_tables) (void)hipFree(ctx->d_tables);
     delete ctx;
     return rc;
   }
@@ -822,6 +1110,7 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
 int be_destroy(be_ctx* ctx) {
   if (!ctx) return BE_OK;
   if (ctx->status) (void)hipFree(ctx->status);
+  if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   delete ctx;
   return BE_OK;
 }
@@ -836,18 +1125,31 @@ static int check_state(be_ctx* ctx, const be_state* st) {
   return BE_OK;
 }
 
-static int launch(be_ctx* ctx, int mode, KArgs& a, void* stream) {
-  if (((uintptr_t)a.out.obs & 15) || ((uintptr_t)a.out.obs_f32 & 15))
+// Per-call KParams: the context's config part + this call's pointers.
+static KParams make_params(be_ctx* ctx, const be_state* st, const be_out* out) {
+  KParams a = ctx->base;
+  a.agent = st->agent; a.goal = st->goal; a.prev_dist = st->prev_dist; a.total_dist = st->total_dist;
+  a.ep_return = st->ep_return; a.ep_len = st->ep_len; a.episode = st->episode; a.static_obs = st->static_obs;
+  a.dyn_obs = st->dyn_obs; a.dyn_goal = st->dyn_goal;
+  if (out) {
+    a.obs = out->obs; a.obs_f32 = out->obs_f32; a.reward = out->reward; a.done = out->done;
+    a.truncated = out->truncated; a.terminal_obs = out->terminal_obs; a.final_return = out->final_return;
+    a.final_len = out->final_len; a.stats = out->stats;
+  }
+  a.tables = ctx->d_tables;
+  a.status = ctx->status;
+  return a;
+}
+
+static int launch(be_ctx* ctx, int mode, KParams& a, void* stream) {
+  if (((uintptr_t)a.obs & 15) || ((uintptr_t)a.obs_f32 & 15))
     return fail(ctx, BE_E_INVALID, "%s", "obs / obs_f32 must be 16-byte aligned");
   int cur = -1;
   HIP_TRY(ctx, hipGetDevice(&cur));
   if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
-  a.c = ctx->cfg;
-  a.t = ctx->tables;
-  a.status = ctx->status;
   const Launch L = pick_kernel(ctx->cfg, mode);
   const int N = ctx->cfg.num_envs;
-  const dim3 grid((unsigned)((N + L.block - 1) / L.block)), block((unsigned)L.block);
+  const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
   hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
   HIP_TRY(ctx, hipGetLastError());
   return BE_OK;
@@ -858,11 +1160,10 @@ int be_reset(be_ctx* ctx, const be_state* st, const uint8_t* mask, const int16_t
   if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
   if (int rc = check_state(ctx, st)) return rc;
   if (reset_tape && tape_len < 0) return fail(ctx, BE_E_INVALID, "%s", "tape_len < 0");
-  KArgs a;
-  memset(&a, 0, sizeof a);
-  a.st = *st;
-  if (out) a.out = *out;
-  if (!a.out.obs && !a.out.obs_f32) return fail(ctx, BE_E_INVALID, "%s", "be_reset needs out->obs or out->obs_f32");
+  if (!out || (!out->obs && !out->obs_f32)) return fail(ctx, BE_E_INVALID, "%s", "be_reset needs out->obs or out->obs_f32");
+  KParams a = make_params(ctx, st, out);
+  a.reward = nullptr; a.done = nullptr; a.truncated = nullptr; a.terminal_obs = nullptr;
+  a.final_return = nullptr; a.final_len = nullptr; a.stats = nullptr;
   a.mask = mask; a.reset_tape = reset_tape; a.reset_tape_len = reset_tape ? tape_len : 0;
   return launch(ctx, MODE_RESET, a, stream);
 }
@@ -873,9 +1174,7 @@ int be_step(be_ctx* ctx, const be_state* st, const uint8_t* actions, const int16
   if (int rc = check_state(ctx, st)) return rc;
   if (!out || !out->reward || !out->done) return fail(ctx, BE_E_INVALID, "%s", "be_step needs out->reward and out->done");
   if (draw_tape && ctx->cfg.autoreset) return fail(ctx, BE_E_INVALID, "%s", "draw tapes (parity mode) need autoreset = 0");
-  KArgs a;
-  memset(&a, 0, sizeof a);
-  a.st = *st; a.out = *out;
+  KParams a = make_params(ctx, st, out);
   a.actions = actions; a.deltas = action_deltas; a.tape = draw_tape;
   return launch(ctx, MODE_STEP, a, stream);
 }
@@ -884,9 +1183,9 @@ int be_observe(be_ctx* ctx, const be_state* st, const be_out* out, void* stream)
   if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
   if (int rc = check_state(ctx, st)) return rc;
   if (!out || (!out->obs && !out->obs_f32)) return fail(ctx, BE_E_INVALID, "%s", "be_observe needs out->obs or out->obs_f32");
-  KArgs a;
-  memset(&a, 0, sizeof a);
-  a.st = *st; a.out = *out;
+  KParams a = make_params(ctx, st, out);
+  a.reward = nullptr; a.done = nullptr; a.truncated = nullptr; a.terminal_obs = nullptr;
+  a.final_return = nullptr; a.final_len = nullptr; a.stats = nullptr;
   return launch(ctx, MODE_OBSERVE, a, stream);
 }
 

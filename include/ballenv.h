@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BE_ABI_VERSION 2
+#define BE_ABI_VERSION 3
 
 #define BE_MAX_STATIC   64
 #define BE_MAX_DYNAMIC  32
@@ -131,9 +131,10 @@ typedef struct be_out {
   uint8_t* terminal_obs;  /* (N, 4+W*W): obs of the terminal state, rows of done envs only (autoreset) */
   double* final_return;   /* (N): episode return, written for done envs only */
   int32_t* final_len;     /* (N): episode length, written for done envs only */
-  double* stats;          /* (8) f64 accumulators: [0]=episodes, [1]=sum return, [2]=sum return^2,
-                             [3]=sum length, [4]=min return, [5]=max return; caller initialises
-                             [4]=+inf [5]=-inf, the rest 0 */
+  double* stats;          /* (be_stats_slots(cfg), 8) f64 accumulators, one slot per block of the step
+                             kernel (no atomics): [0]=episodes, [1]=sum return, [2]=sum return^2,
+                             [3]=sum length, [4]=min return, [5]=max return, [6..7] unused; the caller
+                             initialises [4]=+inf, [5]=-inf, the rest 0, and reduces over slots */
 } be_out;
 
 typedef struct be_ctx be_ctx;
@@ -146,6 +147,8 @@ int be_config_default(be_config* cfg, int32_t num_envs, int32_t window);
 int be_config_check(const be_config* cfg, char* msg, int32_t msg_len);
 /* Bytes of HBM traffic per env-step the step kernel is designed to move (u8 obs). */
 int64_t be_step_bytes(const be_config* cfg);
+/* Number of 8-double slots the be_out.stats buffer must hold for this config. */
+int64_t be_stats_slots(const be_config* cfg);
 const char* be_last_error(const be_ctx* ctx);
 
 /* ---- device functions ---- */

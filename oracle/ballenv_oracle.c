@@ -41,9 +41,14 @@
 #define PHILOX_W1 0xBB67AE85u
 
 /* counter = (global env id, c1, c2, purpose << 24 | sub):
- *   obstacle moves  c1 = episode, c2 = ep_len before the step, sub = obstacle >> 1
+ *   obstacle moves  c1 = episode, c2 = ep_len before the step: obstacle k uses word k & 3
+ *                   of block sub = k >> 2; its draws are randint(n0) = hi32(w*n0), then
+ *                   randint(n1) = hi32(lo32(w*n0)*n1)
  *   sampled action  c1 = episode, c2 = ep_len before the step, sub = 0
- *   reset draw k    c1 = the new episode number, c2 = 0, sub = k >> 2 (word k & 3)
+ *   reset (Philox)  c1 = the new episode number, c2 = 0, one block per quantity:
+ *                   sub = 0: gx, gy, ax, ay | sub = 1 + r: agent re-sample r (ax, ay)
+ *                   sub = 1<<22 | k<<12 | a: static k attempt a (x, y) | sub = 2<<22 | k<<12: dynamic k
+ *   reset (tape)    the reference's single sequential stream
  *   be_sample_actions: c1 = t, c2 = 0                                              */
 enum { PURPOSE_STEP_OBS = 1, PURPOSE_ACTION = 2, PURPOSE_RESET = 3, PURPOSE_SAMPLE = 4 };
 
@@ -103,6 +108,7 @@ static int check_overlap_rect(const be_config* c, int32_t x1, int32_t y1, int32_
 typedef struct {
   const be_config* c;
   const int16_t* tape; int32_t tape_len; int32_t n; int32_t env; int32_t cursor;
+  int32_t word_mode; uint32_t frac;   /* step draws: successive multiply-shifts of one word */
   uint64_t seed; uint32_t gid; uint32_t c1, c2; uint32_t purpose;
   int32_t* status;
 } draw_src;
@@ -110,6 +116,11 @@ typedef struct {
 /* np.random.randint(lo, hi) stand-in */
 static int32_t draw(draw_src* s, int32_t lo, int32_t hi) {
   int32_t k = s->cursor++;
+  if (s->word_mode) {
+    uint64_t prod = (uint64_t)s->frac * (uint64_t)(uint32_t)(hi - lo);
+    s->frac = (uint32_t)prod;
+    return lo + (int32_t)(prod >> 32);
+  }
   if (s->tape) {
     if (k >= s->tape_len) { *s->status |= BE_STATUS_RESET_TAPE_EXHAUSTED; return lo; }
     return s->tape[(int64_t)k * s->n + s->env];
@@ -157,6 +168,51 @@ static void reset_env(const be_config* c, const be_state* st, int32_t i, draw_sr
     st->dyn_goal[(int64_t)k * N + i] = (uint8_t)k;                    /* curr_goal = goal list[k] */
   }
   st->total_dist[i] = calc_dist(ax, ay, gx, gy);                       /* :166 */
+}
+
+/* Perf-mode reset: same rules as reset_env, one Philox block per quantity (see the header comment). */
+static void reset_env_philox(const be_config* c, const be_state* st, int32_t i, uint32_t gid, uint32_t episode,
+                             int32_t* status) {
+  const int32_t N = c->num_envs, W = c->screen_width, H = c->screen_height;
+  uint32_t o[4];
+  uint32_t ctr[4] = {gid, episode, 0u, (uint32_t)PURPOSE_RESET << 24};
+  philox4x32_10(ctr, (uint32_t)c->seed, (uint32_t)(c->seed >> 32), o);
+  int32_t gx = map_range(o[0], W - c->strip_goal_x, W), gy = map_range(o[1], H - c->strip_goal_y, H);
+  int32_t ax = map_range(o[2], 0, c->strip_agent_x), ay = map_range(o[3], 0, c->strip_agent_y);
+  double dist = sqrt(pow((double)(gx - ax), 2.0) + pow((double)(gy - ay), 2.0));
+  for (int32_t r = 0; calc_dist(gx, gy, ax, ay) < c->min_spawn_dist; ++r) {
+    if (r >= REJECT_LIMIT - 1) { *status |= BE_STATUS_REJECTION_LIMIT; break; }
+    ctr[3] = ((uint32_t)PURPOSE_RESET << 24) | (uint32_t)(1 + r);
+    philox4x32_10(ctr, (uint32_t)c->seed, (uint32_t)(c->seed >> 32), o);
+    ax = map_range(o[0], 0, c->strip_agent_x);
+    ay = map_range(o[1], 0, c->strip_agent_y);
+  }
+  st->agent[i] = pk(ax, ay);
+  st->goal[i] = pk(gx, gy);
+  st->prev_dist[i] = dist;
+  st->total_dist[i] = calc_dist(ax, ay, gx, gy);
+  st->ep_return[i] = 0.0;
+  st->ep_len[i] = 0;
+  st->episode[i] = episode;
+  for (int32_t k = 0; k < c->num_static; ++k) {
+    int32_t ox = 0, oy = 0;
+    for (int32_t a = 0;; ++a) {
+      ctr[3] = ((uint32_t)PURPOSE_RESET << 24) | (1u << 22) | ((uint32_t)k << 12) | (uint32_t)a;
+      philox4x32_10(ctr, (uint32_t)c->seed, (uint32_t)(c->seed >> 32), o);
+      ox = map_range(o[0], c->strip_obs_x, W - c->strip_obs_x);
+      oy = map_range(o[1], c->strip_obs_y, H - c->strip_obs_y);
+      if (!check_overlap_rect(c, ox, oy, ax, ay) && !check_overlap_rect(c, ox, oy, gx, gy)) break;
+      if (a >= REJECT_LIMIT - 1) { *status |= BE_STATUS_REJECTION_LIMIT; break; }
+    }
+    st->static_obs[(int64_t)k * N + i] = pk(ox, oy);
+  }
+  for (int32_t k = 0; k < c->num_dynamic; ++k) {
+    ctr[3] = ((uint32_t)PURPOSE_RESET << 24) | (2u << 22) | ((uint32_t)k << 12);
+    philox4x32_10(ctr, (uint32_t)c->seed, (uint32_t)(c->seed >> 32), o);
+    st->dyn_obs[(int64_t)k * N + i] = pk(map_range(o[0], c->strip_obs_x, W - c->strip_obs_x),
+                                        map_range(o[1], c->strip_obs_y, H - c->strip_obs_y));
+    st->dyn_goal[(int64_t)k * N + i] = (uint8_t)k;
+  }
 }
 
 /* prep_state2 + prep_state4 for env i, examples/ball_cnn_ac3.py:330-352, 384-412 */
@@ -249,7 +305,11 @@ int orc_reset(const be_config* c, const be_state* st, const uint8_t* mask, const
               int32_t tape_len, const be_out* out, int32_t* status) {
   for (int32_t i = 0; i < c->num_envs; ++i) {
     if (mask && !mask[i]) continue;
-    draw_src ds = {c, tape, tape_len, c->num_envs, i, 0, c->seed,
+    if (!tape) {
+      reset_env_philox(c, st, i, (uint32_t)(c->env_offset + i), st->episode[i] + 1u, status);
+      continue;
+    }
+    draw_src ds = {c, tape, tape_len, c->num_envs, i, 0, 0, 0u, c->seed,
                    (uint32_t)(c->env_offset + i), st->episode[i] + 1u, 0u, PURPOSE_RESET, status};
     reset_env(c, st, i, &ds);
   }
@@ -291,8 +351,9 @@ int orc_step(const be_config* c, const be_state* st, const uint8_t* actions,
     int32_t counter = st->ep_len[i] % (c->goal_change_step + 1);
     for (int32_t k = 0; k < c->num_dynamic; ++k) {
       /* tape: rows (k*2 + d, N) of this step's (Nd, 2, N) tape.
-       * Philox: draw d of obstacle k is word 2*(k&1)+d of block sub=k>>1, i.e. cursor 2k+d. */
-      draw_src ds = {c, tape ? tape + (int64_t)k * 2 * N : NULL, 2, N, i, tape ? 0 : 2 * k,
+       * Philox: both draws from word k&3 of block k>>2 (successive multiply-shifts). */
+      draw_src ds = {c, tape ? tape + (int64_t)k * 2 * N : NULL, 2, N, i, 0, tape ? 0 : 1,
+                     tape ? 0u : philox_word(c->seed, gid, episode, len0, PURPOSE_STEP_OBS, (uint32_t)k >> 2, k & 3),
                      c->seed, gid, episode, len0, PURPOSE_STEP_OBS, status};
       move_obstacle(c, st, i, k, counter, &ds);
     }
@@ -328,8 +389,7 @@ int orc_step(const be_config* c, const be_state* st, const uint8_t* actions,
       if (out->stats) stats_add(out->stats, st->ep_return[i], len);
       if (c->autoreset) {
         if (out->terminal_obs) observe_env(c, st, i, out->terminal_obs + (int64_t)i * F);
-        draw_src ds = {c, NULL, 0, N, i, 0, c->seed, gid, episode + 1u, 0u, PURPOSE_RESET, status};
-        reset_env(c, st, i, &ds);
+        reset_env_philox(c, st, i, gid, episode + 1u, status);
       }
     }
     if (out->obs) {

@@ -213,7 +213,7 @@ def test_vs_oracle_philox_autoreset(gpu, W, N):
         np.testing.assert_array_equal(info["final_len"].cpu().numpy()[d], out["final_len"][d.astype(bool)])
         np.testing.assert_array_equal(info["terminal_obs"].cpu().numpy(), out["terminal_obs"])
         assert_state_equal(env, st, f"t={t}")
-    s_gpu = env.stats_buf.cpu().numpy()
+    s_gpu = env.stats_record().cpu().numpy()
     s_orc = out["stats"]
     assert s_gpu[0] == s_orc[0] and s_gpu[4] == s_orc[4] and s_gpu[5] == s_orc[5] and s_gpu[3] == s_orc[3]
     np.testing.assert_allclose(s_gpu[1:3], s_orc[1:3], rtol=1e-12, atol=1e-9)

@@ -1,0 +1,64 @@
+// Diagnostics: per-wave phase timeline of one be_step launch (needs the -DBE_DIAG_STAMPS library in tools/diag).
+// build: hipcc --offload-arch=gfx950 -O3 -I include tools/stamps.hip -L tools/diag -lballenv -Wl,-rpath,'$ORIGIN/diag' -o tools/stamps
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <vector>
+#include "ballenv.h"
+extern "C" int be_diag_stamps(unsigned long long* rt, unsigned long long* cy);
+extern "C" int be_diag_clear(void);
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+constexpr int DW = 1 << 16, DP = 12;
+static double pct(std::vector<double> v, double p) { if (v.empty()) return 0; std::sort(v.begin(), v.end()); return v[(size_t)(p * (v.size() - 1))]; }
+int main(int argc, char** argv) {
+  int N = argc > 1 ? atoi(argv[1]) : 65536;
+  be_config cfg; be_config_default(&cfg, N, 10);
+  be_ctx* ctx = nullptr;
+  if (be_create(&cfg, 0, &ctx)) { printf("create: %s\n", be_last_error(nullptr)); return 1; }
+  be_state st; be_out out; memset(&st, 0, sizeof st); memset(&out, 0, sizeof out);
+  CK(hipMalloc(&st.agent, 4 * N)); CK(hipMalloc(&st.goal, 4 * N)); CK(hipMalloc(&st.prev_dist, 8 * N));
+  CK(hipMalloc(&st.total_dist, 8 * N)); CK(hipMalloc(&st.ep_return, 8 * N)); CK(hipMalloc(&st.ep_len, 4 * N));
+  CK(hipMalloc(&st.episode, 4 * N)); CK(hipMalloc(&st.static_obs, 4 * 13 * N)); CK(hipMalloc(&st.dyn_obs, 4 * 5 * N));
+  CK(hipMalloc(&st.dyn_goal, 5 * N)); CK(hipMalloc(&out.obs, 104 * N)); CK(hipMalloc(&out.reward, 8 * N)); CK(hipMalloc(&out.done, N));
+  CK(hipMemset(st.episode, 0, 4 * N)); CK(hipMemset(st.ep_len, 0, 4 * N));
+  uint8_t* acts; CK(hipMalloc(&acts, (size_t)N * 64));
+  be_sample_actions(ctx, acts, 64, 7, nullptr);
+  be_reset(ctx, &st, nullptr, nullptr, 0, &out, nullptr);
+  for (int k = 0; k < 300; ++k) be_step(ctx, &st, acts + (size_t)(k % 64) * N, nullptr, nullptr, &out, nullptr);
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned long long> rt(DW * DP), cy(DW * DP);
+  for (int rep = 0; rep < 3; ++rep) {
+    be_diag_clear();
+    be_step(ctx, &st, acts + (size_t)(rep % 64) * N, nullptr, nullptr, &out, nullptr);
+    CK(hipDeviceSynchronize());
+    be_diag_stamps(rt.data(), cy.data());
+    int waves = 0; unsigned long long t0 = ~0ull, t1 = 0;
+    for (int w = 0; w < DW; ++w) if (rt[w * DP + 0]) { waves++; t0 = std::min(t0, rt[w * DP + 0]); t1 = std::max(t1, rt[w * DP + 6]); }
+    std::vector<double> start, endt; std::vector<std::vector<double>> ph(6);
+    for (int w = 0; w < DW; ++w) {
+      if (!rt[w * DP + 0]) continue;
+      start.push_back((rt[w * DP + 0] - t0) * 0.01); endt.push_back((rt[w * DP + 6] - t0) * 0.01);
+      for (int p = 0; p < 6; ++p) ph[p].push_back((double)(cy[w * DP + p + 1] - cy[w * DP + p]));
+    }
+    printf("rep %d: N=%d waves=%d span(first start..last end)=%.2f us\n", rep, N, waves, (t1 - t0) * 0.01);
+    printf("  wave start us: p0 %.2f p50 %.2f p90 %.2f max %.2f | wave end us: p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
+           pct(start, 0), pct(start, .5), pct(start, .9), pct(start, 1), pct(endt, .1), pct(endt, .5), pct(endt, .9), pct(endt, 1));
+    const char* names[6] = {"entry->barrier1 (loads)", "barrier1->physics", "physics->stats/reset", "reset->stage", "stage->barrier2", "barrier2->end(copy)"};
+    for (int p = 0; p < 6; ++p)
+      printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", names[p], pct(ph[p], .5), pct(ph[p], .9), pct(ph[p], .99), pct(ph[p], 1));
+    std::vector<std::vector<double>> sub(4);
+    for (int w = 0; w < DW; ++w) {
+      if (!rt[w * DP + 0] || !cy[w * DP + 8]) continue;
+      sub[0].push_back((double)(cy[w * DP + 8] - cy[w * DP + 1]));
+      sub[1].push_back((double)(cy[w * DP + 9] - cy[w * DP + 8]));
+      sub[2].push_back((double)(cy[w * DP + 10] - cy[w * DP + 9]));
+      sub[3].push_back((double)(cy[w * DP + 2] - cy[w * DP + 10]));
+    }
+    const char* sn[4] = {"  physics: action+move", "  physics: dynamic obs", "  physics: static obs", "  physics: reward+stores"};
+    for (int p = 0; p < 4; ++p)
+      printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", sn[p], pct(sub[p], .5), pct(sub[p], .9), pct(sub[p], .99), pct(sub[p], 1));
+  }
+  return 0;
+}
