@@ -94,10 +94,16 @@ struct KParams {
   int32_t reset_tape_len;
 };
 
-// Diagnostic phase-skip bits (timing ablations only; outputs are wrong when set).
+// Diagnostic phase-skip bits (timing ablations only; outputs are wrong when set).  Only
+// diagnostics builds (-DBE_DIAG_STAMPS or -DBE_DIAG_SKIP) read them; in production DBG(x) is 0.
 enum : uint32_t { DBG_NO_STATS = 1, DBG_NO_RASTER = 2, DBG_NO_OBS = 4, DBG_NO_PHILOX = 8, DBG_NO_DYN = 16,
                   DBG_NO_NEAR = 32, DBG_EXIT_ENTRY = 64, DBG_EXIT_BARRIER = 128, DBG_EXIT_PHYSICS = 256,
                   DBG_EXIT_RASTER = 512 };
+#if defined(BE_DIAG_STAMPS) || defined(BE_DIAG_SKIP)
+#define DBG(x) (p.dbg & (x))
+#else
+#define DBG(x) 0
+#endif
 
 // Diagnostics-only build (-DBE_DIAG_STAMPS): per-wave phase stamps for tools/microbench.
 #ifdef BE_DIAG_STAMPS
@@ -139,6 +145,8 @@ struct u4 { uint32_t x, y, z, w; };
 // Philox4x32-10 (Salmon et al., SC'11); same as oracle/ballenv_oracle.c
 __device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, unsigned long long seed) {
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  // keep the key schedule in VGPRs: hoisted into SGPRs it pins 20 scalar registers and spills
+  asm volatile("" : "+v"(k0), "+v"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
@@ -492,6 +500,9 @@ __device__ __forceinline__ WaveStats wave_stats(bool done, double ret, int len) 
 // ------------------------------------------------------------------ lane groups
 // LPE lanes cooperate on one env: obstacle k belongs to lane k % LPE, obs word w to lane w % LPE.
 constexpr int BLOCK_THREADS = 256;
+#ifndef BE_LPE
+#define BE_LPE 1
+#endif
 template <int LPE>
 __device__ __forceinline__ uint32_t group_or(uint32_t x) {
   static_assert(LPE == 1 || LPE == 2 || LPE == 4, "LPE must be 1, 2 or 4");
@@ -506,15 +517,17 @@ __device__ __forceinline__ int group_bcast(int x) {  // value of the group's lan
   else return __builtin_amdgcn_update_dpp(0, x, 0x00, 0xF, 0xF, false);                          // quad_perm 0,0,0,0
 }
 
-constexpr int lanes_for(int WT) { return WT == 0 ? 1 : 4; }
+constexpr int lanes_for(int WT) { return WT == 0 ? 1 : BE_LPE; }
 constexpr int envs_per_block(int WT) { return BLOCK_THREADS / lanes_for(WT); }
+constexpr int RCAP = 64;  // resets handled per cooperative pass (more loop)
 
 // One dynamic obstacle's move_obstacles (ballenv_env.py:323-353).  Tape mode: t0/t1
 // are the values of its first/second randint call.  Philox mode: both draws come
 // from one 32-bit word w -- randint(n0) = hi32(w*n0), then randint(n1) =
 // hi32(lo32(w*n0)*n1) (the multiply-shift's fractional part).
-__device__ __forceinline__ void dyn_move(const KParams& p, const Tables& t, int64_t a, int& ox, int& oy, int gi,
-                                         int speed, bool change, bool tape, int t0, int t1, uint32_t w) {
+__device__ __forceinline__ void dyn_move(const KParams& p, const Tables& t, int32_t* pos, uint8_t* goal_ix, int& ox,
+                                         int& oy, int gi, int speed, bool change, bool tape, int t0, int t1,
+                                         uint32_t w) {
   if (!change) {
     const int32_t gp = t.goal[gi];
     const int tx = px(gp) - ox, ty = py(gp) - oy;
@@ -534,37 +547,103 @@ __device__ __forceinline__ void dyn_move(const KParams& p, const Tables& t, int6
     }
     ox += mx * speed; oy += my * speed;
     if (ox < -32768 || ox > 32767 || oy < -32768 || oy > 32767) atomicOr(p.status, BE_STATUS_COORD_RANGE);
-    p.dyn_obs[a] = pk(ox, oy);
+    *pos = pk(ox, oy);
   } else {  // new goal from the other goals; no move this step (Q5)
     const int n_other = t.n_other[gi];
     if (n_other == 0) atomicOr(p.status, BE_STATUS_NO_GOAL);
-    else p.dyn_goal[a] = t.other[gi][tape ? t0 : (int)__umulhi(w, (uint32_t)n_other)];
+    else *goal_ix = t.other[gi][tape ? t0 : (int)__umulhi(w, (uint32_t)n_other)];
+  }
+}
+
+// Window-box pre-filter: an obstacle can light a cell only if it lies in the cell box grown by R.
+struct NearBox {
+  int bx0, by0; uint32_t bw, bh;
+  __device__ explicit NearBox(const Win& g)
+      : bx0(g.x0 - g.R), by0(g.y0 - g.R), bw((uint32_t)(g.sx * (g.w - 1) + 2 * g.R)),
+        bh((uint32_t)(g.sy * (g.kr - 1) + 2 * g.R)) {}
+  __device__ __forceinline__ bool maybe(int ox, int oy) const {
+    return (uint32_t)(ox - bx0) <= bw && (uint32_t)(oy - by0) <= bh;
+  }
+};
+
+__device__ __forceinline__ bool collides(int ox, int oy, int ax, int ay, uint32_t R2) {
+  const int dx = ox - ax, dy = oy - ay;  // |d| < 2^17: 24-bit multiplies are exact
+  return (uint32_t)__mul24(dx, dx) + (uint32_t)__mul24(dy, dy) <= R2;
+}
+
+// Rasterise ONE obstacle into row masks with LDS atomic OR (cooperative reset path).
+template <int WT>
+__device__ void raster_one_lds(uint32_t* rows, const Win& g, int f, int e) {
+  constexpr int K = Geo<WT>::K;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int ady = abs(e - g.sy * k);
+    if (ady <= g.R) {
+      const int hw = isqrt_small(g.R2 - ady * ady);
+      int lo, hi;
+      if (g.sx == 1) { lo = f - hw; hi = f + hw; }
+      else { lo = -floordiv(hw - f, g.sx); hi = floordiv(f + hw, g.sx); }
+      lo = max(lo, 0); hi = min(hi, WT - 1);
+      if (lo <= hi) atomicOr(&rows[k], (2u << hi) - (1u << lo));
+    }
+  }
+}
+
+// Write one env's obs row (all F bytes) into the LDS stage from row masks (one thread).
+template <int WT>
+__device__ void stage_full_row(uint8_t* dst, const uint32_t (&flat)[Geo<WT>::NW], int quad) {
+  constexpr int F = Geo<WT>::F;
+  if constexpr ((F & 3) == 0) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    d[0] = 1u << (8 * quad);
+#pragma unroll
+    for (int w = 1; w < F / 4; ++w) {
+      const int jc = 4 * (w - 1);
+      d[w] = (((flat[jc >> 5] >> (jc & 31)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < F; ++b) dst[b] = (uint8_t)obs_byte<WT>(flat, quad, b);
   }
 }
 
 // ------------------------------------------------------------------ the kernel
 // MODE_STEP: physics + (autoreset) + obs.  MODE_RESET: reset masked envs + obs.
-// MODE_OBSERVE: obs only.  WT = compile-time W (0 = runtime W, no LDS staging).
-// LPE = lanes per env (4 for compiled W): at 65536 envs that is 4 waves per SIMD
-// instead of 1, so the waves hide each other's memory and ALU latency.
+// MODE_OBSERVE: obs only.  WT = compile-time W (0 = runtime W: no LDS staging,
+// sequential resets).  LPE = lanes per env.
+//
+// Resets (Philox mode) are block-cooperative: envs that must reset are compacted
+// into an LDS list, then phase A draws each one's goal/agent (one thread per env)
+// and phase B draws every obstacle of every listed env (one thread per obstacle),
+// rasterising it straight into the env's LDS row masks.  A finishing env therefore
+// costs the block ~2 Philox blocks of latency instead of a serial ~20 on one lane.
 template <int WT, int MODE>
 __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   constexpr int LPE = lanes_for(WT);
   constexpr int EPB = envs_per_block(WT);
   constexpr int SPL = CS / LPE, DPL = CD / LPE;   // obstacle slots per lane in the register chunk
+  constexpr bool COOP = WT > 0;                   // cooperative reset path (needs compile-time W)
+  constexpr int KR = WT > 0 ? Geo<WT>::K : 1;
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Tables t;
   __shared__ WaveStats s_ws[BLOCK_THREADS / 64];
+  __shared__ int s_nreset;
+  __shared__ int16_t s_slot_of[EPB];               // env -> reset slot (-1: none)
+  __shared__ int16_t s_reset_el[RCAP];
+  __shared__ uint32_t s_reset_ep[RCAP];
+  __shared__ int32_t s_reset_agent[RCAP], s_reset_goal[RCAP];
+  __shared__ uint32_t s_rows[RCAP][KR];
   constexpr int TW = (int)(sizeof(Tables) / 4);
   static_assert(TW <= BLOCK_THREADS && sizeof(Tables) % 4 == 0, "table staging assumes <= 256 words");
 
   DIAG(0);
-  if (p.dbg & DBG_EXIT_ENTRY) return;
+  if (DBG(DBG_EXIT_ENTRY)) return;
   const int N = p.n, Ns = p.ns, Nd = p.nd;
   const int tid = threadIdx.x;
   const int q = tid & (LPE - 1);                  // lane within the env's group
   const int el = tid / LPE;                        // env within the block
-  const int i = blockIdx.x * EPB + el;
+  const int blk0 = (int)blockIdx.x * EPB;
+  const int i = blk0 + el;
   const bool valid = i < N;
   const bool lead = q == 0;                        // the group lane that owns per-env stores
 
@@ -605,24 +684,26 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
         const int k = q + LPE * j;
-        if (k < ns0) so[j] = p.static_obs[(int64_t)k * N + i];
+        if (k < ns0) so[j] = (p.static_obs + (size_t)k * N)[i];
       }
 #pragma unroll
       for (int j = 0; j < DPL; ++j) {
         const int k = q + LPE * j;
         if (k < nd0) {
-          dp[j] = p.dyn_obs[(int64_t)k * N + i];
-          dgi[j] = p.dyn_goal[(int64_t)k * N + i];
-          if (p.tape) { t0[j] = p.tape[(int64_t)(2 * k) * N + i]; t1[j] = p.tape[(int64_t)(2 * k + 1) * N + i]; }
+          dp[j] = (p.dyn_obs + (size_t)k * N)[i];
+          dgi[j] = (p.dyn_goal + (size_t)k * N)[i];
+          if (p.tape) { t0[j] = (p.tape + (size_t)(2 * k) * N)[i]; t1[j] = (p.tape + (size_t)(2 * k + 1) * N)[i]; }
         }
       }
     }
     if (MODE != MODE_OBSERVE) episode = p.episode[i];
   }
   if (tid < TW) reinterpret_cast<uint32_t*>(&t)[tid] = tword;
-  __syncthreads();  // the block's first barrier: tables staged, all loads above have landed
+  if (tid < EPB) s_slot_of[tid] = -1;
+  if (tid == 0) s_nreset = 0;
+  __syncthreads();  // barrier 1: tables staged, all loads above have landed
   DIAG(1);
-  if (p.dbg & DBG_EXIT_BARRIER) {
+  if (DBG(DBG_EXIT_BARRIER)) {
     if (valid && (agent0 ^ goal0 ^ so[0] ^ dp[0] ^ (int)len0 ^ (int)old_dist) == 0x7fffffff) p.obs[i] = 1;
     return;
   }
@@ -641,6 +722,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       ax = min(max(px(agent0) + p.speed_x * dx, 0), p.screen_w);
       ay = min(max(py(agent0) + p.speed_y * dy, 0), p.screen_h);
       const Win g(p, ax, ay);
+      const NearBox nb(g);
       const uint32_t R2 = (uint32_t)g.R2;
       bool hs = false, hd = false;
       DIAG(8);
@@ -652,26 +734,33 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       if (counter > p.goal_change) counter -= p.goal_change + 1;
       const bool change = counter >= p.goal_change;
       const bool tape = p.tape != nullptr;
-      // Philox words: obstacle k uses word k&3 of block k>>2.  With 4 lanes per env every
-      // lane computes ONE block (block = lane parity) and the pair swaps words by DPP.
+      // Philox words: obstacle k uses word k&3 of block k>>2 (both of its draws).
       uint32_t wj[DPL];
 #pragma unroll
       for (int j = 0; j < DPL; ++j) wj[j] = 0u;
-      if (!tape && !(p.dbg & DBG_NO_PHILOX)) {
-        if constexpr (LPE == 4) {
+      if (!tape && !DBG(DBG_NO_PHILOX)) {
+        if constexpr (LPE == 4) {  // one block per lane (= lane parity), words swapped by DPP
           const u4 blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(q & 1)), p.seed);
           const uint32_t own = pick_word(blk, q), send = pick_word(blk, q ^ 1);
           const uint32_t recv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xF, 0xF, false);
           wj[0] = (q & 1) ? recv : own;   // k = q     : block 0, word q
           wj[1] = (q & 1) ? own : recv;   // k = q + 4 : block 1, word q
+        } else if constexpr (LPE == 2) {  // lane q: k = q + 2j -> block j>>1, word q + 2(j&1); lane q computes block q
+          const u4 blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)q), p.seed);
+          // block0 words: k=0..3 (lane0: k0,k2 = w0,w2; lane1: k1,k3 = w1,w3); block1: k=4..7
+          const uint32_t s0 = q ? blk.x : blk.y, s1 = q ? blk.z : blk.w;   // words the partner needs
+          const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s0, 0xB1, 0xF, 0xF, false);
+          const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0xB1, 0xF, 0xF, false);
+          // lane0 has block0 (w0..w3), receives block1 w0,w2; lane1 has block1, receives block0 w1,w3
+          wj[0] = q ? r0 : blk.x;   // k = q      block 0 word q
+          wj[1] = q ? r1 : blk.z;   // k = q + 2  block 0 word q + 2
+          wj[2] = q ? blk.y : r0;   // k = q + 4  block 1 word q
+          wj[3] = q ? blk.w : r1;   // k = q + 6  block 1 word q + 2
         } else {
-          u4 blk{0, 0, 0, 0};
-#pragma unroll
-          for (int j = 0; j < DPL; ++j) {
-            const int k = q + LPE * j;
-            if (((k & 3) == 0 || j == 0) && k < nd0) blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(k >> 2)), p.seed);
-            wj[j] = pick_word(blk, k & 3);
-          }
+          u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+          u4 b1 = nd0 > 4 ? philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 1u), p.seed) : u4{0, 0, 0, 0};
+          wj[0] = b0.x; wj[1] = b0.y; wj[2] = b0.z; wj[3] = b0.w;
+          wj[4 % DPL] = b1.x; wj[5 % DPL] = b1.y; wj[6 % DPL] = b1.z; wj[7 % DPL] = b1.w;
         }
       }
 #pragma unroll
@@ -679,22 +768,24 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         const int k = q + LPE * j;
         if (k < nd0) {
           int ox = px(dp[j]), oy = py(dp[j]);
-          if (!(p.dbg & DBG_NO_DYN))
-            dyn_move(p, t, (int64_t)k * N + i, ox, oy, dgi[j], t.speed[k], change, tape, t0[j], t1[j], wj[j]);
-          hd |= d2u(ox - ax, oy - ay) <= R2;
+          if (!DBG(DBG_NO_DYN))
+            dyn_move(p, t, p.dyn_obs + (size_t)k * N + i, p.dyn_goal + (size_t)k * N + i, ox, oy, dgi[j], t.speed[k],
+                     change, tape, t0[j], t1[j], wj[j]);
+          hd |= collides(ox, oy, ax, ay, R2);
           int f, e;
-          if (g.near(ox, oy, f, e) && !(p.dbg & DBG_NO_NEAR)) nl.push(f, e);
+          if (nb.maybe(ox, oy) && g.near(ox, oy, f, e) && !DBG(DBG_NO_NEAR)) nl.push(f, e);
         }
       }
       for (int kb = CD + q; kb < Nd; kb += LPE) {  // configs with more than CD dynamic obstacles
-        const int64_t aa = (int64_t)kb * N + i;
-        int ox = px(p.dyn_obs[aa]), oy = py(p.dyn_obs[aa]);
+        int32_t* pos = p.dyn_obs + (size_t)kb * N + i;
+        int ox = px(*pos), oy = py(*pos);
         const u4 blk = tape ? u4{0, 0, 0, 0} : philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(kb >> 2)), p.seed);
-        const int tt0 = tape ? p.tape[(int64_t)(2 * kb) * N + i] : 0, tt1 = tape ? p.tape[(int64_t)(2 * kb + 1) * N + i] : 0;
-        dyn_move(p, t, aa, ox, oy, p.dyn_goal[aa], t.speed[kb], change, tape, tt0, tt1, pick_word(blk, kb & 3));
-        hd |= d2u(ox - ax, oy - ay) <= R2;
+        const int tt0 = tape ? (p.tape + (size_t)(2 * kb) * N)[i] : 0, tt1 = tape ? (p.tape + (size_t)(2 * kb + 1) * N)[i] : 0;
+        dyn_move(p, t, pos, p.dyn_goal + (size_t)kb * N + i, ox, oy, (p.dyn_goal + (size_t)kb * N)[i], t.speed[kb],
+                 change, tape, tt0, tt1, pick_word(blk, kb & 3));
+        hd |= collides(ox, oy, ax, ay, R2);
         int f, e;
-        if (g.near(ox, oy, f, e)) nl.push(f, e);
+        if (nb.maybe(ox, oy) && g.near(ox, oy, f, e)) nl.push(f, e);
       }
       DIAG(9);
       // ---- static obstacles: collision + near test
@@ -703,23 +794,23 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         const int k = q + LPE * j;
         if (k < ns0) {
           const int ox = px(so[j]), oy = py(so[j]);
-          hs |= d2u(ox - ax, oy - ay) <= R2;
+          hs |= collides(ox, oy, ax, ay, R2);
           int f, e;
-          if (g.near(ox, oy, f, e) && !(p.dbg & DBG_NO_NEAR)) nl.push(f, e);
+          if (nb.maybe(ox, oy) && g.near(ox, oy, f, e) && !DBG(DBG_NO_NEAR)) nl.push(f, e);
         }
       }
       for (int kb = CS + q; kb < Ns; kb += LPE) {
-        const int32_t o = p.static_obs[(int64_t)kb * N + i];
+        const int32_t o = (p.static_obs + (size_t)kb * N)[i];
         const int ox = px(o), oy = py(o);
-        hs |= d2u(ox - ax, oy - ay) <= R2;
+        hs |= collides(ox, oy, ax, ay, R2);
         int f, e;
-        if (g.near(ox, oy, f, e)) nl.push(f, e);
+        if (nb.maybe(ox, oy) && g.near(ox, oy, f, e)) nl.push(f, e);
       }
       // the group's collision flags (every lane of a valid group is active here)
       hs = group_or<LPE>((uint32_t)hs) != 0u;
       hd = group_or<LPE>((uint32_t)hd) != 0u;
-
       DIAG(10);
+
       // ---- distance, reward, done (ballenv_env.py:268-286, 200-229)
       const double dist = calc_dist(gx, gy, ax, ay);
       double reward = 0.0 - p.time_penalty;
@@ -750,19 +841,20 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     }
   }
   DIAG(2);
-  if (p.dbg & DBG_EXIT_PHYSICS) return;
+  if (DBG(DBG_EXIT_PHYSICS)) return;
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
-  if (MODE == MODE_STEP && p.stats && !(p.dbg & DBG_NO_STATS))
+  if (MODE == MODE_STEP && p.stats && !DBG(DBG_NO_STATS))
     ws = wave_stats(done && lead, fin_ret, fin_len);  // all lanes converged here
 
-  // ---- episode boundary: terminal obs + reset (rare; the whole group takes the branch)
+  // ---- episode boundary
   bool do_reset = false;
   if (valid) {
     if (MODE == MODE_STEP) do_reset = done && p.autoreset;
     if (MODE == MODE_RESET) do_reset = p.mask ? (p.mask[i] != 0) : true;
   }
+  const bool tape_reset = MODE == MODE_RESET && p.reset_tape != nullptr;
   if (valid && do_reset) {
-    if (MODE == MODE_STEP && p.terminal_obs) {
+    if (MODE == MODE_STEP && p.terminal_obs) {  // obs of the terminal state (group-uniform branch)
       const int F = 4 + p.window * p.window;
       const Win g(p, ax, ay);
       const int quad = quadrant(ax, ay, gx, gy);
@@ -777,51 +869,56 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         write_row_generic<BLOCK_THREADS>(nl, g, quad, p.terminal_obs + (int64_t)i * F, nullptr);
       }
     }
-    if (MODE == MODE_RESET && p.reset_tape) {
-      // parity mode: the reference's single sequential draw stream, on the lead lane
+    if (!COOP || tape_reset) {
+      // sequential reset on the lead lane: the reference's single draw stream (tape), or runtime-W kernels
       if (lead) {
-        ResetDraws ds{p.reset_tape, p.reset_tape_len, N, i, 0, gid, episode + 1u, p.seed, p.status};
-        reset_env<BLOCK_THREADS>(p, t, i, ds, ax, ay, gx, gy, nl);   // lead lane's list gets every obstacle
+        ResetDraws ds{tape_reset ? p.reset_tape : nullptr, p.reset_tape_len, N, i, 0, gid, episode + 1u, p.seed,
+                      p.status};
+        if (tape_reset) reset_env<BLOCK_THREADS>(p, t, i, ds, ax, ay, gx, gy, nl);
+        else reset_env_philox<BLOCK_THREADS, 1>(p, t, i, 0, gid, episode + 1u, ax, ay, gx, gy, nl);
       } else {
         nl.cnt = 0;
       }
       ax = group_bcast<LPE>(ax); ay = group_bcast<LPE>(ay);
       gx = group_bcast<LPE>(gx); gy = group_bcast<LPE>(gy);
-    } else {
-      reset_env_philox<BLOCK_THREADS, LPE>(p, t, i, q, gid, episode + 1u, ax, ay, gx, gy, nl);
+    } else if (lead) {
+      const int slot = atomicAdd(&s_nreset, 1);   // LDS atomic: compact the block's resets
+      s_slot_of[el] = (int16_t)slot;
+      if (slot < RCAP) { s_reset_el[slot] = (int16_t)el; s_reset_ep[slot] = episode + 1u; }
     }
   } else if (valid && MODE != MODE_STEP) {
     // observe / reset of an unmasked env: near list of the current state, split over the group
     const Win g(p, ax, ay);
     for (int k = q; k < Ns; k += LPE) {
-      const int32_t o = p.static_obs[(int64_t)k * N + i];
+      const int32_t o = (p.static_obs + (size_t)k * N)[i];
       int f, e;
       if (g.near(px(o), py(o), f, e)) nl.push(f, e);
     }
     for (int k = q; k < Nd; k += LPE) {
-      const int32_t o = p.dyn_obs[(int64_t)k * N + i];
+      const int32_t o = (p.dyn_obs + (size_t)k * N)[i];
       int f, e;
       if (g.near(px(o), py(o), f, e)) nl.push(f, e);
     }
   }
-
   DIAG(3);
+
   // ---- observation (prep_state4)
   if constexpr (WT > 0) {
     constexpr int F = Geo<WT>::F;
+    // 1) envs that did not go through the cooperative reset: their own near lists
     uint32_t flat[Geo<WT>::NW];
     int quad = 0;
     if (valid) {
       const Win g(p, ax, ay);
       uint32_t rows[Geo<WT>::K];
-      if (p.dbg & DBG_NO_RASTER) nl.cnt = 0;
+      if (DBG(DBG_NO_RASTER)) nl.cnt = 0;
       raster_rows<WT, BLOCK_THREADS>(nl, g, rows);
 #pragma unroll
       for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k]);
       flatten<WT>(rows, flat);
       quad = quadrant(ax, ay, gx, gy);
     }
-    if (p.dbg & (DBG_NO_OBS | DBG_EXIT_RASTER)) {
+    if (DBG(DBG_NO_OBS | DBG_EXIT_RASTER)) {
       if (valid && flat[0] == 0x12345u && quad == 7) p.obs[i] = 1;   // keep the rows live
       return;
     }
@@ -836,8 +933,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
             if (w == 0) v = 1u << (8 * quad);
             else {
               const int jc = 4 * (w - 1);  // first cell of this word (nibble aligned)
-              const uint32_t nib = (flat[jc >> 5] >> (jc & 31)) & 0xFu;
-              v = (nib * 0x00204081u) & 0x01010101u;
+              v = (((flat[jc >> 5] >> (jc & 31)) & 0xFu) * 0x00204081u) & 0x01010101u;
             }
             dst[w] = v;
           }
@@ -853,10 +949,102 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     }
     if (MODE == MODE_STEP && (tid & 63) == 0) s_ws[tid >> 6] = ws;
     DIAG(4);
-    __syncthreads();  // stage complete
+    __syncthreads();  // barrier 2: stage written; reset list complete
+
+    // 2) cooperative resets (Philox): overwrite the stage rows of the listed envs
+    if (COOP && !tape_reset) {
+      const int nres = s_nreset;   // block-uniform
+      for (int r0 = 0; r0 < nres; r0 += RCAP) {
+        const int nr = min(RCAP, nres - r0);
+        if (r0 > 0) {   // more than RCAP resets in this block (e.g. reset of every env): refill the list
+          if (valid && lead && s_slot_of[el] >= r0 && s_slot_of[el] < r0 + RCAP) {
+            const int s = s_slot_of[el] - r0;
+            s_reset_el[s] = (int16_t)el; s_reset_ep[s] = episode + 1u;
+          }
+          __syncthreads();
+        }
+        // phase A: goal / agent (one thread per env), per-env scalars, clear row masks
+        if (tid < nr) {
+          const int e_l = s_reset_el[tid];
+          const int ir = blk0 + e_l;
+          const uint32_t ep = s_reset_ep[tid];
+          const uint32_t g_id = (uint32_t)p.gid0 + (uint32_t)ir;
+          const int W = p.screen_w, H = p.screen_h;
+          const u4 b0 = philox(g_id, ep, 0u, tag(PURPOSE_RESET, 0), p.seed);
+          const int rgx = map_range(b0.x, W - t.strip_goal_x, W), rgy = map_range(b0.y, H - t.strip_goal_y, H);
+          int rax = map_range(b0.z, 0, t.strip_agent_x), ray = map_range(b0.w, 0, t.strip_agent_y);
+          const double dist = calc_dist(rgx, rgy, rax, ray);
+          for (int r = 0; calc_dist(rgx, rgy, rax, ray) < p.min_spawn_dist; ++r) {   // :121-126
+            if (r >= REJECT_LIMIT - 1) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+            const u4 b = philox(g_id, ep, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
+            rax = map_range(b.x, 0, t.strip_agent_x); ray = map_range(b.y, 0, t.strip_agent_y);
+          }
+          p.agent[ir] = pk(rax, ray);
+          p.goal[ir] = pk(rgx, rgy);
+          p.prev_dist[ir] = dist;  // pre-resample distance (Q9)
+          p.total_dist[ir] = calc_dist(rax, ray, rgx, rgy);
+          p.ep_return[ir] = 0.0;
+          p.ep_len[ir] = 0;
+          p.episode[ir] = ep;
+          s_reset_agent[tid] = pk(rax, ray);
+          s_reset_goal[tid] = pk(rgx, rgy);
+#pragma unroll
+          for (int k = 0; k < KR; ++k) s_rows[tid][k] = 0u;
+        }
+        __syncthreads();
+        // phase B: every obstacle of every listed env, one per thread
+        const int per = Ns + Nd;
+        const int R = t.radius_obstacle + t.radius_agent;
+        const int rx = R, ry2 = t.radius_obstacle + 2 * t.radius_agent;
+        for (int it = tid; it < nr * per; it += BLOCK_THREADS) {
+          const int s = it / per, k = it - s * per;
+          const int ir = blk0 + s_reset_el[s];
+          const uint32_t ep = s_reset_ep[s];
+          const uint32_t g_id = (uint32_t)p.gid0 + (uint32_t)ir;
+          const int rax = px(s_reset_agent[s]), ray = py(s_reset_agent[s]);
+          const int rgx = px(s_reset_goal[s]), rgy = py(s_reset_goal[s]);
+          const int W = p.screen_w, H = p.screen_h;
+          int ox, oy;
+          if (k < Ns) {   // static: rejection vs agent/goal rectangles (:131-149, :193-197)
+            for (int at = 0;; ++at) {
+              const u4 b = philox(g_id, ep, 0u, tag(PURPOSE_RESET, (1u << 22) | ((uint32_t)k << 12) | (uint32_t)at), p.seed);
+              ox = map_range(b.x, t.strip_obs_x, W - t.strip_obs_x);
+              oy = map_range(b.y, t.strip_obs_y, H - t.strip_obs_y);
+              const bool ra = abs(ox - rax) < rx && 2 * abs(oy - ray) < ry2;
+              const bool rg = abs(ox - rgx) < rx && 2 * abs(oy - rgy) < ry2;
+              if (!ra && !rg) break;
+              if (at >= REJECT_LIMIT - 1) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+            }
+            (p.static_obs + (size_t)k * N)[ir] = pk(ox, oy);
+          } else {        // dynamic (:153-164)
+            const int kd = k - Ns;
+            const u4 b = philox(g_id, ep, 0u, tag(PURPOSE_RESET, (2u << 22) | ((uint32_t)kd << 12)), p.seed);
+            ox = map_range(b.x, t.strip_obs_x, W - t.strip_obs_x);
+            oy = map_range(b.y, t.strip_obs_y, H - t.strip_obs_y);
+            (p.dyn_obs + (size_t)kd * N)[ir] = pk(ox, oy);
+            (p.dyn_goal + (size_t)kd * N)[ir] = (uint8_t)kd;
+          }
+          const Win g(p, rax, ray);
+          int f, e;
+          if (g.near(ox, oy, f, e)) raster_one_lds<WT>(s_rows[s], g, f, e);
+        }
+        __syncthreads();
+        // phase C: the listed envs' obs rows into the stage
+        if (tid < nr) {
+          uint32_t rows[Geo<WT>::K], fl[Geo<WT>::NW];
+#pragma unroll
+          for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = s_rows[tid][k];
+          flatten<WT>(rows, fl);
+          const int e_l = s_reset_el[tid];
+          const int32_t ag = s_reset_agent[tid], go = s_reset_goal[tid];
+          stage_full_row<WT>(stage + e_l * F, fl, quadrant(px(ag), py(ag), px(go), py(go)));
+        }
+        __syncthreads();
+      }
+    }
     DIAG(5);
-    const int nvalid = min(EPB, N - (int)blockIdx.x * EPB);
-    copy_out<BLOCK_THREADS>(stage, F, nvalid, (int64_t)blockIdx.x * EPB, p.obs, p.obs_f32);
+    const int nvalid = min(EPB, N - blk0);
+    copy_out<BLOCK_THREADS>(stage, F, nvalid, (int64_t)blk0, p.obs, p.obs_f32);
   } else {
     if (valid && lead) {
       const int F = 4 + p.window * p.window;

@@ -45,7 +45,7 @@ int main(int argc, char** argv) {
     printf("rep %d: N=%d waves=%d span(first start..last end)=%.2f us\n", rep, N, waves, (t1 - t0) * 0.01);
     printf("  wave start us: p0 %.2f p50 %.2f p90 %.2f max %.2f | wave end us: p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
            pct(start, 0), pct(start, .5), pct(start, .9), pct(start, 1), pct(endt, .1), pct(endt, .5), pct(endt, .9), pct(endt, 1));
-    const char* names[6] = {"entry->barrier1 (loads)", "barrier1->physics", "physics->stats/reset", "reset->stage", "stage->barrier2", "barrier2->end(copy)"};
+    const char* names[6] = {"entry->barrier1 (loads)", "barrier1->physics", "physics->reset list", "list->stage written", "stage->after coop reset", "coop reset->end(copy)"};
     for (int p = 0; p < 6; ++p)
       printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", names[p], pct(ph[p], .5), pct(ph[p], .9), pct(ph[p], .99), pct(ph[p], 1));
     std::vector<std::vector<double>> sub(4);
