@@ -149,8 +149,9 @@ __device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint
   asm volatile("" : "+v"(k0), "+v"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    // one v_mad_u64_u32 per product instead of a mul_hi + mul_lo pair
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
@@ -228,6 +229,9 @@ struct NearList {
     base[cnt * BLOCK] = (uint32_t)(f & 0xFFFF) | ((uint32_t)e << 16);
     ++cnt;
   }
+  __device__ __forceinline__ void push_if(bool c, int f, int e) {
+    if (c) push(f, e);   // (an unconditional write + predicated count measured no faster)
+  }
   __device__ __forceinline__ void get(int n, int& f, int& e) const {
     const uint32_t v = base[n * BLOCK];
     f = (int)(int16_t)(v & 0xFFFF); e = (int)v >> 16;
@@ -249,16 +253,24 @@ __device__ __forceinline__ void raster_rows(const NearList<BLOCK>& nl, const Win
   for (int n = 0; n < nl.cnt; ++n) {
     int f, e;
     nl.get(n, f, e);
+    if (g.sx == 1) {  // branch-free span per row
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int ady = abs(e - g.sy * k);
-      if (ady <= g.R) {
-        const int hw = isqrt_small(g.R2 - ady * ady);
-        int lo, hi;
-        if (g.sx == 1) { lo = f - hw; hi = f + hw; }
-        else { lo = -floordiv(hw - f, g.sx); hi = floordiv(f + hw, g.sx); }
-        lo = max(lo, 0); hi = min(hi, WT - 1);
-        if (lo <= hi) rows[k] |= (2u << hi) - (1u << lo);
+      for (int k = 0; k < K; ++k) {
+        const int ady = abs(e - g.sy * k);
+        const bool in = ady <= g.R;
+        const int hw = isqrt_small(in ? g.R2 - ady * ady : 0);
+        const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
+        rows[k] |= (in && lo <= hi) ? (2u << hi) - (1u << lo) : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int ady = abs(e - g.sy * k);
+        if (ady <= g.R) {
+          const int hw = isqrt_small(g.R2 - ady * ady);
+          const int lo = max(-floordiv(hw - f, g.sx), 0), hi = min(floordiv(f + hw, g.sx), WT - 1);
+          if (lo <= hi) rows[k] |= (2u << hi) - (1u << lo);
+        }
       }
     }
   }
@@ -521,38 +533,35 @@ constexpr int lanes_for(int WT) { return WT == 0 ? 1 : BE_LPE; }
 constexpr int envs_per_block(int WT) { return BLOCK_THREADS / lanes_for(WT); }
 constexpr int RCAP = 64;  // resets handled per cooperative pass (more loop)
 
-// One dynamic obstacle's move_obstacles (ballenv_env.py:323-353).  Tape mode: t0/t1
-// are the values of its first/second randint call.  Philox mode: both draws come
-// from one 32-bit word w -- randint(n0) = hi32(w*n0), then randint(n1) =
-// hi32(lo32(w*n0)*n1) (the multiply-shift's fractional part).
-__device__ __forceinline__ void dyn_move(const KParams& p, const Tables& t, int32_t* pos, uint8_t* goal_ix, int& ox,
-                                         int& oy, int gi, int speed, bool change, bool tape, int t0, int t1,
-                                         uint32_t w) {
-  if (!change) {
-    const int32_t gp = t.goal[gi];
-    const int tx = px(gp) - ox, ty = py(gp) - oy;
-    int mv;  // -1 = directed move toward the current goal
-    if (tx != 0 && ty != 0) {
-      const int u = tape ? t0 : (int)__umulhi(w, 100u);
-      mv = u < p.certainty ? -1 : (tape ? t1 : (int)__umulhi(w * 100u, 9u));
-    } else {
-      mv = tape ? t0 : (int)__umulhi(w, 9u);
-    }
-    int mx, my;
-    if (mv < 0) { mx = tx > 0 ? 1 : -1; my = ty > 0 ? 1 : -1; }
-    else {  // move_list of ballenv_env.py:324: (-1,-1) twice, no (-1,0) (Q4)
-      mx = mv < 3 ? 1 : (mv < 6 ? 0 : -1);
-      const int r3 = mv - 3 * (mv / 3);
-      my = mv == 8 ? -1 : (r3 == 0 ? 1 : (r3 == 1 ? -1 : 0));
-    }
-    ox += mx * speed; oy += my * speed;
-    if (ox < -32768 || ox > 32767 || oy < -32768 || oy > 32767) atomicOr(p.status, BE_STATUS_COORD_RANGE);
-    *pos = pk(ox, oy);
-  } else {  // new goal from the other goals; no move this step (Q5)
-    const int n_other = t.n_other[gi];
-    if (n_other == 0) atomicOr(p.status, BE_STATUS_NO_GOAL);
-    else *goal_ix = t.other[gi][tape ? t0 : (int)__umulhi(w, (uint32_t)n_other)];
-  }
+// One dynamic obstacle's move_obstacles (ballenv_env.py:323-353), branch-free.
+// Tape mode: t0/t1 are the values of its first/second randint call.  Philox mode:
+// both draws come from one 32-bit word w -- randint(n0) = hi32(w*n0), then
+// randint(n1) = hi32(lo32(w*n0)*n1) (the multiply-shift's fractional part).
+// Returns the new goal index (== gi unless a goal change picked another one).
+// move_list of ballenv_env.py:324, (dx+1, dy+1) packed 2 bits per entry:
+// (1,1) (1,-1) (1,0) (0,1) (0,-1) (0,0) (-1,1) (-1,-1) (-1,-1) -- (-1,-1) twice, no (-1,0) (Q4)
+constexpr uint32_t OBS_MX = (2u << 0) | (2u << 2) | (2u << 4) | (1u << 6) | (1u << 8) | (1u << 10) | (0u << 12) | (0u << 14) | (0u << 16);
+constexpr uint32_t OBS_MY = (2u << 0) | (0u << 2) | (1u << 4) | (2u << 6) | (0u << 8) | (1u << 10) | (2u << 12) | (0u << 14) | (0u << 16);
+__device__ __forceinline__ int dyn_move(const KParams& p, const Tables& t, int& ox, int& oy, int gi, int speed,
+                                        bool change, bool tape, int t0, int t1, uint32_t w, uint32_t& flags) {
+  const int32_t gp = t.goal[gi];
+  const int tx = px(gp) - ox, ty = py(gp) - oy;
+  const bool both = (tx != 0) & (ty != 0);
+  const int u = tape ? t0 : (int)__umulhi(w, 100u);
+  const int m = tape ? (both ? t1 : t0) : (int)__umulhi(both ? w * 100u : w, 9u);
+  const bool directed = both & (u < p.certainty);
+  const int mx = directed ? (tx > 0 ? 1 : -1) : (int)((OBS_MX >> (2 * m)) & 3u) - 1;
+  const int my = directed ? (ty > 0 ? 1 : -1) : (int)((OBS_MY >> (2 * m)) & 3u) - 1;
+  const int nx = ox + mx * speed, ny = oy + my * speed;
+  // goal change (no move this step, Q5): newGoalList pick
+  const int n_other = t.n_other[gi];
+  const int pick = tape ? t0 : (int)__umulhi(w, (uint32_t)n_other);
+  const int ng = t.other[gi][min(pick, BE_MAX_GOALS - 1)];
+  flags |= (change && n_other == 0) ? (uint32_t)BE_STATUS_NO_GOAL : 0u;
+  flags |= (!change && (nx < -32768 || nx > 32767 || ny < -32768 || ny > 32767)) ? (uint32_t)BE_STATUS_COORD_RANGE : 0u;
+  ox = change ? ox : nx;
+  oy = change ? oy : ny;
+  return (change && n_other > 0) ? ng : gi;
 }
 
 // Window-box pre-filter: an obstacle can light a cell only if it lies in the cell box grown by R.
@@ -656,6 +665,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   double fin_ret = 0.0;
   int fin_len = 0;
   uint32_t episode = 0;
+  uint32_t st_flags = 0;   // BE_STATUS_* raised by this lane, published once per wave
   const uint32_t gid = (uint32_t)p.gid0 + (uint32_t)i;
 
   // ---- phase 0: issue every load of this env (independent, coalesced across the wave)
@@ -681,15 +691,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       total = p.total_dist[i];
       ret = p.ep_return[i];
       len0 = p.ep_len[i];
+      // fixed slots: indices past the count re-read the last obstacle (same lines: no extra traffic)
+      if (ns0 > 0) {
 #pragma unroll
-      for (int j = 0; j < SPL; ++j) {
-        const int k = q + LPE * j;
-        if (k < ns0) so[j] = (p.static_obs + (size_t)k * N)[i];
+        for (int j = 0; j < SPL; ++j) so[j] = (p.static_obs + (size_t)min(q + LPE * j, ns0 - 1) * N)[i];
       }
+      if (nd0 > 0) {
 #pragma unroll
-      for (int j = 0; j < DPL; ++j) {
-        const int k = q + LPE * j;
-        if (k < nd0) {
+        for (int j = 0; j < DPL; ++j) {
+          const int k = min(q + LPE * j, nd0 - 1);
           dp[j] = (p.dyn_obs + (size_t)k * N)[i];
           dgi[j] = (p.dyn_goal + (size_t)k * N)[i];
           if (p.tape) { t0[j] = (p.tape + (size_t)(2 * k) * N)[i]; t1[j] = (p.tape + (size_t)(2 * k + 1) * N)[i]; }
@@ -713,7 +723,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     if (MODE == MODE_STEP) {
       // ---- action -> agent move + clamp (ballenv_env.py:247-259); every lane of the group
       if (p.actions) {
-        if (a >= p.num_actions) { if (lead) atomicOr(p.status, BE_STATUS_BAD_ACTION); a = 0; }
+        st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
+        a = a < p.num_actions ? a : 0;
         const int32_t m = t.action[a]; dx = px(m); dy = py(m);
       } else if (!p.deltas) {  // sampled actions
         const u4 b = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_ACTION, 0), p.seed);
@@ -747,42 +758,49 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
           wj[1] = (q & 1) ? own : recv;   // k = q + 4 : block 1, word q
         } else if constexpr (LPE == 2) {  // lane q: k = q + 2j -> block j>>1, word q + 2(j&1); lane q computes block q
           const u4 blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)q), p.seed);
-          // block0 words: k=0..3 (lane0: k0,k2 = w0,w2; lane1: k1,k3 = w1,w3); block1: k=4..7
           const uint32_t s0 = q ? blk.x : blk.y, s1 = q ? blk.z : blk.w;   // words the partner needs
           const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s0, 0xB1, 0xF, 0xF, false);
           const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0xB1, 0xF, 0xF, false);
-          // lane0 has block0 (w0..w3), receives block1 w0,w2; lane1 has block1, receives block0 w1,w3
           wj[0] = q ? r0 : blk.x;   // k = q      block 0 word q
           wj[1] = q ? r1 : blk.z;   // k = q + 2  block 0 word q + 2
           wj[2] = q ? blk.y : r0;   // k = q + 4  block 1 word q
           wj[3] = q ? blk.w : r1;   // k = q + 6  block 1 word q + 2
         } else {
-          u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
-          u4 b1 = nd0 > 4 ? philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 1u), p.seed) : u4{0, 0, 0, 0};
+          const u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
           wj[0] = b0.x; wj[1] = b0.y; wj[2] = b0.z; wj[3] = b0.w;
-          wj[4 % DPL] = b1.x; wj[5 % DPL] = b1.y; wj[6 % DPL] = b1.z; wj[7 % DPL] = b1.w;
+          if (nd0 > 4) {
+            const u4 b1 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 1u), p.seed);
+            wj[4 % DPL] = b1.x; wj[5 % DPL] = b1.y; wj[6 % DPL] = b1.z; wj[7 % DPL] = b1.w;
+          }
         }
       }
+      // fixed slot loops: slots past the obstacle count hold a far-away sentinel, so the
+      // collision / window tests are branch-free; only their stores are skipped
+      constexpr int FAR = -30000;
 #pragma unroll
       for (int j = 0; j < DPL; ++j) {
         const int k = q + LPE * j;
-        if (k < nd0) {
-          int ox = px(dp[j]), oy = py(dp[j]);
-          if (!DBG(DBG_NO_DYN))
-            dyn_move(p, t, p.dyn_obs + (size_t)k * N + i, p.dyn_goal + (size_t)k * N + i, ox, oy, dgi[j], t.speed[k],
-                     change, tape, t0[j], t1[j], wj[j]);
-          hd |= collides(ox, oy, ax, ay, R2);
-          int f, e;
-          if (nb.maybe(ox, oy) && g.near(ox, oy, f, e) && !DBG(DBG_NO_NEAR)) nl.push(f, e);
+        const bool real = k < nd0;
+        int ox = real ? px(dp[j]) : FAR, oy = real ? py(dp[j]) : FAR;
+        if (!DBG(DBG_NO_DYN) && real) {
+          const int ng = dyn_move(p, t, ox, oy, dgi[j], t.speed[k], change, tape, t0[j], t1[j], wj[j], st_flags);
+          (p.dyn_obs + (size_t)k * N)[i] = pk(ox, oy);
+          if (ng != dgi[j]) (p.dyn_goal + (size_t)k * N)[i] = (uint8_t)ng;
         }
+        hd |= collides(ox, oy, ax, ay, R2);
+        int f, e;
+        nl.push_if(nb.maybe(ox, oy) && g.near(ox, oy, f, e) && !DBG(DBG_NO_NEAR), f, e);
       }
       for (int kb = CD + q; kb < Nd; kb += LPE) {  // configs with more than CD dynamic obstacles
         int32_t* pos = p.dyn_obs + (size_t)kb * N + i;
+        uint8_t* gp = p.dyn_goal + (size_t)kb * N + i;
         int ox = px(*pos), oy = py(*pos);
+        const int gi = *gp;
         const u4 blk = tape ? u4{0, 0, 0, 0} : philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(kb >> 2)), p.seed);
         const int tt0 = tape ? (p.tape + (size_t)(2 * kb) * N)[i] : 0, tt1 = tape ? (p.tape + (size_t)(2 * kb + 1) * N)[i] : 0;
-        dyn_move(p, t, pos, p.dyn_goal + (size_t)kb * N + i, ox, oy, (p.dyn_goal + (size_t)kb * N)[i], t.speed[kb],
-                 change, tape, tt0, tt1, pick_word(blk, kb & 3));
+        const int ng = dyn_move(p, t, ox, oy, gi, t.speed[kb], change, tape, tt0, tt1, pick_word(blk, kb & 3), st_flags);
+        *pos = pk(ox, oy);
+        if (ng != gi) *gp = (uint8_t)ng;
         hd |= collides(ox, oy, ax, ay, R2);
         int f, e;
         if (nb.maybe(ox, oy) && g.near(ox, oy, f, e)) nl.push(f, e);
@@ -792,12 +810,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
         const int k = q + LPE * j;
-        if (k < ns0) {
-          const int ox = px(so[j]), oy = py(so[j]);
-          hs |= collides(ox, oy, ax, ay, R2);
-          int f, e;
-          if (nb.maybe(ox, oy) && g.near(ox, oy, f, e) && !DBG(DBG_NO_NEAR)) nl.push(f, e);
-        }
+        const bool real = k < ns0;
+        const int ox = real ? px(so[j]) : FAR, oy = real ? py(so[j]) : FAR;
+        hs |= collides(ox, oy, ax, ay, R2);
+        int f, e;
+        nl.push_if(nb.maybe(ox, oy) && g.near(ox, oy, f, e) && !DBG(DBG_NO_NEAR), f, e);
       }
       for (int kb = CS + q; kb < Ns; kb += LPE) {
         const int32_t o = (p.static_obs + (size_t)kb * N)[i];
@@ -842,6 +859,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   }
   DIAG(2);
   if (DBG(DBG_EXIT_PHYSICS)) return;
+  if (MODE == MODE_STEP && __ballot(st_flags != 0u)) {   // rare: OR the wave's flags, one atomic
+    uint32_t f = st_flags;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
+    if ((tid & 63) == 0) atomicOr(p.status, (int)f);
+  }
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   if (MODE == MODE_STEP && p.stats && !DBG(DBG_NO_STATS))
     ws = wave_stats(done && lead, fin_ret, fin_len);  // all lanes converged here
