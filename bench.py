@@ -17,8 +17,10 @@ Timed region: the K steps replayed from HIP graphs of captured be_step
 launches (Philox draws are keyed by per-env state -- env id, episode,
 ep_len -- so replays are fresh steps), bracketed by barrier + synchronize,
 max over ranks.
-Kernel duration for the roofline: HIP events around each of K eager launches
-of the same kernel on the same stream, right after the timed region.
+Kernel duration for the roofline: HIP events recorded on the replay stream
+around the timed region (K back-to-back be_kernel launches, nothing else on the
+stream) -> average per launch; it includes the small inter-launch gap, so it is
+an upper bound on the kernel duration that rocprofv3 reports.
 CPU baseline (rank 0, N=1 only, before any GPU work): oracle/py_ballenv.py,
 the reference's algorithm restated in scalar Python, one process per core.
 """
@@ -131,16 +133,19 @@ def main():
             graphs.append(g)
         torch.cuda.synchronize(dev)
 
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     if args.mode == "graph":
         for g in graphs:
-            g.replay()
+            g.replay()            # replays on the current stream (= stream)
     else:
         for t in range(K):
             launch(t, s_ptr)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -155,31 +160,21 @@ def main():
         ep = env.episode_stats()
     env.status()
 
-    # kernel duration: HIP events around each eager launch on the launch stream
-    KD = min(K, 200)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(KD)]
-    for t in range(KD):
-        evs[t][0].record(stream)
-        launch(t, s_ptr)
-        evs[t][1].record(stream)
-    torch.cuda.synchronize(dev)
-    durs = sorted(a.elapsed_time(b) for a, b in evs)           # ms
-    kern_ms = sum(durs) / len(durs)
-    kern_med = durs[len(durs) // 2]
+    # average launch duration over the timed region (events on the launch stream)
+    kern_ms = ev0.elapsed_time(ev1) / K
 
     total_steps = K * N * world
     value = total_steps / elapsed
     achieved = B * N / (kern_ms * 1e-3) / 1e9                  # GB/s, algorithmic, per launch
 
-    traffic = None
+    # HBM-side bytes per launch from the committed PMC passes (tools/pmc_bench.sh):
+    # 2 x FETCH_SIZE (gfx950 reports half of wide reads) + WRITE_SIZE, same kernel / envs / W
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     if os.path.exists(pmc):
-        try:
-            d = json.load(open(pmc))
-            if d.get("envs") == N and d.get("window") == W:
-                traffic = d.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+        d = json.load(open(pmc))
+        if d.get("envs") == N and d.get("window") == W:
+            traffic, traffic_src = d.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT)
 
     if rank == 0:
         line = {
@@ -194,8 +189,8 @@ def main():
                        "launch": "hipGraph replay of be_step launches" if args.mode == "graph" else "eager"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_env_step": B, "kernel_ms_mean": kern_ms, "kernel_ms_median": kern_med,
-                         "kernel": "be_kernel<10, MODE_STEP>"},
+                         "bytes_per_env_step": B, "kernel_us_mean": kern_ms * 1e3,
+                         "kernel": f"be_kernel<{W}, 0> (MODE_STEP)", "traffic_source": traffic_src},
             "cpu_baseline": base,
             "episodes": ep,
         }

@@ -26,3 +26,7 @@ if [ "${PROFILE:-1}" = "1" ]; then
       python bench.py --no-cpu-baseline --steps 300 --warmup 20 ${BENCH_ARGS:-}
   find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \;
 fi
+if [ "${PMC:-1}" = "1" ]; then
+  step pmc 700 bash tools/pmc_bench.sh
+  tail -1 gpurun_out/pmc.log
+fi
