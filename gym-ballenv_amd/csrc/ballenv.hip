@@ -56,6 +56,7 @@ constexpr uint32_t PURPOSE_STEP_OBS = 1, PURPOSE_ACTION = 2, PURPOSE_RESET = 3, 
 constexpr int REJECT_LIMIT = 4096;
 constexpr int CS = 16;  // static obstacles per register chunk
 constexpr int CD = 8;   // dynamic obstacles per register chunk
+constexpr int HW_MAX = 63;   // largest collision radius R with a half-width table
 
 enum Mode { MODE_STEP = 0, MODE_RESET = 1, MODE_OBSERVE = 2 };
 
@@ -68,6 +69,7 @@ struct Tables {
   int32_t radius_obstacle, radius_agent;
   uint8_t n_other[BE_MAX_GOALS];              // goals with a different value than goal g
   uint8_t other[BE_MAX_GOALS][BE_MAX_GOALS];  // pick -> goal index, per current goal g (newGoalList)
+  uint8_t hw[HW_MAX + 1];                     // floor(sqrt(R^2 - d^2)), d = 0..R (only when R <= HW_MAX)
 };
 
 // Kernel arguments: hot fields first, 64-byte lines (see the latency notes above).
@@ -162,6 +164,14 @@ __device__ __forceinline__ uint32_t tag(uint32_t purpose, uint32_t sub) { return
 __device__ __forceinline__ uint32_t pick_word(const u4& b, int w) {
   return w == 0 ? b.x : (w == 1 ? b.y : (w == 2 ? b.z : b.w));
 }
+// 24-bit field j (0..4) of a Philox block read as x | y<<32 | z<<64 | w<<96
+__device__ __forceinline__ uint32_t pick_field(const u4& b, int j) {
+  constexpr uint32_t M = 0xFFFFFFu;
+  return j == 0 ? (b.x & M)
+       : j == 1 ? (__builtin_amdgcn_alignbit(b.y, b.x, 24) & M)
+       : j == 2 ? (__builtin_amdgcn_alignbit(b.z, b.y, 16) & M)
+       : j == 3 ? (b.z >> 8) : (b.w & M);
+}
 // uniform integer in [lo, hi) from one 32-bit word (multiply-shift)
 __device__ __forceinline__ int map_range(uint32_t r, int lo, int hi) {
   return lo + (int)__umulhi(r, (uint32_t)(hi - lo));
@@ -244,12 +254,28 @@ template <int WT> struct Geo {
   static constexpr int F = 4 + WT * WT;
 };
 
-// Rasterise the near list into K row bitmasks (compile-time W).
-template <int WT, int BLOCK>
-__device__ __forceinline__ void raster_rows(const NearList<BLOCK>& nl, const Win& g, uint32_t (&rows)[Geo<WT>::K]) {
+// Rasterise the near list into K row bitmasks (compile-time W).  HWT: unit cell step and
+// R <= HW_MAX, so a row's half-width comes from the LDS table instead of an isqrt.
+template <int WT, int BLOCK, bool HWT = false>
+__device__ __forceinline__ void raster_rows(const NearList<BLOCK>& nl, const Win& g, uint32_t (&rows)[Geo<WT>::K],
+                                            const uint8_t* hwt = nullptr) {
   constexpr int K = Geo<WT>::K;
 #pragma unroll
   for (int k = 0; k < K; ++k) rows[k] = 0u;
+  if constexpr (HWT) {
+    for (int n = 0; n < nl.cnt; ++n) {
+      int f, e;
+      nl.get(n, f, e);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int ady = abs(e - k);
+        const int hw = hwt[min(ady, HW_MAX)];
+        const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
+        rows[k] |= (ady <= g.R && lo <= hi) ? (2u << hi) - (1u << lo) : 0u;
+      }
+    }
+    return;
+  }
   for (int n = 0; n < nl.cnt; ++n) {
     int f, e;
     nl.get(n, f, e);
@@ -496,16 +522,18 @@ struct WaveStats { double n, s1, s2, sl, mn, mx; };
 
 __device__ __forceinline__ WaveStats wave_stats(bool done, double ret, int len) {
   WaveStats w{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
-  const unsigned long long m = __ballot(done);
-  if (m == 0ull) return w;  // wave-uniform: nobody finished (the common case)
-  double s1 = done ? ret : 0.0, s2 = done ? ret * ret : 0.0, sl = done ? (double)len : 0.0;
-  double mn = done ? ret : INFINITY, mx = done ? ret : -INFINITY;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    s1 += __shfl_xor(s1, o); s2 += __shfl_xor(s2, o); sl += __shfl_xor(sl, o);
-    mn = fmin(mn, __shfl_xor(mn, o)); mx = fmax(mx, __shfl_xor(mx, o));
+  // wave-uniform loop over the finished lanes in lane order (deterministic; ~1 per wave per
+  // step at the reference's episode lengths, so a few readlanes beat a 6-level shuffle tree)
+  for (unsigned long long m = __ballot(done); m; m &= m - 1) {
+    const int l = __ffsll((long long)m) - 1;
+    const unsigned long long bits = __double_as_longlong(ret);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), l);
+    const double r = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+    const int n = __builtin_amdgcn_readlane(len, l);
+    w.n += 1.0; w.s1 += r; w.s2 += r * r; w.sl += (double)n;
+    w.mn = fmin(w.mn, r); w.mx = fmax(w.mx, r);
   }
-  w.n = (double)__popcll(m); w.s1 = s1; w.s2 = s2; w.sl = sl; w.mn = mn; w.mx = mx;
   return w;
 }
 
@@ -535,8 +563,9 @@ constexpr int RCAP = 64;  // resets handled per cooperative pass (more loop)
 
 // One dynamic obstacle's move_obstacles (ballenv_env.py:323-353), branch-free.
 // Tape mode: t0/t1 are the values of its first/second randint call.  Philox mode:
-// both draws come from one 32-bit word w -- randint(n0) = hi32(w*n0), then
-// randint(n1) = hi32(lo32(w*n0)*n1) (the multiply-shift's fractional part).
+// both draws come from one 24-bit field f -- randint(n0) = (f*n0) >> 24, then
+// randint(n1) = (((f*n0) mod 2^24) * n1) >> 24 (the multiply-shift's fractional part;
+// n0, n1 <= 128, so every product fits 32 bits and runs on the full-rate 24-bit multiplier).
 // Returns the new goal index (== gi unless a goal change picked another one).
 // move_list of ballenv_env.py:324, (dx+1, dy+1) packed 2 bits per entry:
 // (1,1) (1,-1) (1,0) (0,1) (0,-1) (0,0) (-1,1) (-1,-1) (-1,-1) -- (-1,-1) twice, no (-1,0) (Q4)
@@ -547,20 +576,47 @@ __device__ __forceinline__ int dyn_move(const KParams& p, const Tables& t, int& 
   const int32_t gp = t.goal[gi];
   const int tx = px(gp) - ox, ty = py(gp) - oy;
   const bool both = (tx != 0) & (ty != 0);
-  const int u = tape ? t0 : (int)__umulhi(w, 100u);
-  const int m = tape ? (both ? t1 : t0) : (int)__umulhi(both ? w * 100u : w, 9u);
+  const uint32_t p1 = __umul24(w, 100u);
+  const int u = tape ? t0 : (int)(p1 >> 24);
+  const int m = tape ? (both ? t1 : t0) : (int)(__umul24(both ? (p1 & 0xFFFFFFu) : w, 9u) >> 24);
   const bool directed = both & (u < p.certainty);
   const int mx = directed ? (tx > 0 ? 1 : -1) : (int)((OBS_MX >> (2 * m)) & 3u) - 1;
   const int my = directed ? (ty > 0 ? 1 : -1) : (int)((OBS_MY >> (2 * m)) & 3u) - 1;
   const int nx = ox + mx * speed, ny = oy + my * speed;
   // goal change (no move this step, Q5): newGoalList pick
   const int n_other = t.n_other[gi];
-  const int pick = tape ? t0 : (int)__umulhi(w, (uint32_t)n_other);
+  const int pick = tape ? t0 : (int)(__umul24(w, (uint32_t)n_other) >> 24);
   const int ng = t.other[gi][min(pick, BE_MAX_GOALS - 1)];
   flags |= (change && n_other == 0) ? (uint32_t)BE_STATUS_NO_GOAL : 0u;
   flags |= (!change && (nx < -32768 || nx > 32767 || ny < -32768 || ny > 32767)) ? (uint32_t)BE_STATUS_COORD_RANGE : 0u;
   ox = change ? ox : nx;
   oy = change ? oy : ny;
+  return (change && n_other > 0) ? ng : gi;
+}
+
+// Philox-mode dyn_move for the fixed-shape kernels, written as straight-line integer code so
+// the scheduler can interleave the obstacles (select by mask, no divergent regions).
+// Returns the goal index after the step; (ox, oy) is moved unless change.
+__device__ __forceinline__ int dyn_move_philox(const KParams& p, const Tables& t, int& ox, int& oy, int gi, int speed,
+                                               bool change, uint32_t f, uint32_t& flags) {
+  const int32_t gp = t.goal[gi];
+  const int n_other = t.n_other[gi];
+  const int tx = px(gp) - ox, ty = py(gp) - oy;
+  const bool both = (tx != 0) & (ty != 0);
+  const uint32_t p1 = __umul24(f, 100u);
+  const uint32_t src = both ? (p1 & 0xFFFFFFu) : f;
+  const uint32_t m2 = 2u * (__umul24(src, 9u) >> 24);            // 2 * OBS_MOVES index
+  const bool directed = both & ((int)(p1 >> 24) < p.certainty);
+  const int sx = (tx > 0) - (tx < 0), sy = (ty > 0) - (ty < 0);
+  const int rx = (int)((OBS_MX >> m2) & 3u) - 1, ry = (int)((OBS_MY >> m2) & 3u) - 1;
+  const int mx = directed ? sx : rx, my = directed ? sy : ry;
+  const int step = change ? 0 : speed;                             // goal change: no move (Q5)
+  const int nx = ox + mx * step, ny = oy + my * step;
+  const int pick = (int)(__umul24(f, (uint32_t)n_other) >> 24);
+  const int ng = t.other[gi][min(pick, BE_MAX_GOALS - 1)];
+  flags |= (change && n_other == 0) ? (uint32_t)BE_STATUS_NO_GOAL : 0u;
+  flags |= ((uint32_t)(nx + 32768) > 65535u || (uint32_t)(ny + 32768) > 65535u) ? (uint32_t)BE_STATUS_COORD_RANGE : 0u;
+  ox = nx; oy = ny;
   return (change && n_other > 0) ? ng : gi;
 }
 
@@ -626,11 +682,17 @@ __device__ void stage_full_row(uint8_t* dst, const uint32_t (&flat)[Geo<WT>::NW]
 // and phase B draws every obstacle of every listed env (one thread per obstacle),
 // rasterising it straight into the env's LDS row masks.  A finishing env therefore
 // costs the block ~2 Philox blocks of latency instead of a serial ~20 on one lane.
-template <int WT, int MODE>
+//
+// NSC/NDC > 0: a step kernel specialised for exactly NSC static / NDC dynamic obstacles in
+// Philox mode (no tape), one lane per env -- every obstacle loop is unrolled to its exact
+// trip count (the dispatcher picks it only for a matching config).
+template <int WT, int MODE, int NSC = 0, int NDC = 0>
 __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
-  constexpr int LPE = lanes_for(WT);
-  constexpr int EPB = envs_per_block(WT);
-  constexpr int SPL = CS / LPE, DPL = CD / LPE;   // obstacle slots per lane in the register chunk
+  constexpr bool FIXED = NSC > 0 || NDC > 0;
+  constexpr int LPE = FIXED ? 1 : lanes_for(WT);
+  constexpr int EPB = BLOCK_THREADS / LPE;
+  static_assert(!FIXED || (MODE == MODE_STEP && WT > 0 && NSC <= CS && NDC <= CD), "fixed-shape kernels: step only");
+  constexpr int SPL = FIXED ? NSC : CS / LPE, DPL = FIXED ? NDC : CD / LPE;   // obstacle slots per lane
   constexpr bool COOP = WT > 0;                   // cooperative reset path (needs compile-time W)
   constexpr int KR = WT > 0 ? Geo<WT>::K : 1;
   extern __shared__ __align__(16) uint8_t smem[];
@@ -647,7 +709,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
 
   DIAG(0);
   if (DBG(DBG_EXIT_ENTRY)) return;
-  const int N = p.n, Ns = p.ns, Nd = p.nd;
+  const int N = p.n, Ns = FIXED ? NSC : p.ns, Nd = FIXED ? NDC : p.nd;
   const int tid = threadIdx.x;
   const int q = tid & (LPE - 1);                  // lane within the env's group
   const int el = tid / LPE;                        // env within the block
@@ -656,9 +718,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   const bool valid = i < N;
   const bool lead = q == 0;                        // the group lane that owns per-env stores
 
-  // LDS: [near lists: nobs slots x 256 lanes x 4 B][obs stage: EPB x F bytes]
+  // LDS: [near lists: nobs+1 slots x 256 lanes x 4 B][obs stage: EPB x F bytes]
   NearList<BLOCK_THREADS> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
-  uint8_t* stage = smem + (size_t)(Ns + Nd) * BLOCK_THREADS * 4;
+  uint8_t* stage = smem + (size_t)(Ns + Nd + 1) * BLOCK_THREADS * 4;
 
   int ax = 0, ay = 0, gx = 0, gy = 0;
   bool done = false;
@@ -673,43 +735,68 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   int a = 0, dx = 0, dy = 0, len0 = 0;
   int32_t agent0 = 0, goal0 = 0;
   double old_dist = 0.0, total = 1.0, ret = 0.0;
-  const int ns0 = min(Ns, CS), nd0 = min(Nd, CD);
+  const int ns0 = FIXED ? NSC : min(Ns, CS), nd0 = FIXED ? NDC : min(Nd, CD);
   int32_t so[SPL], dp[DPL];
   int dgi[DPL], t0[DPL], t1[DPL];
 #pragma unroll
   for (int j = 0; j < SPL; ++j) so[j] = 0;
 #pragma unroll
   for (int j = 0; j < DPL; ++j) { dp[j] = 0; dgi[j] = 0; t0[j] = 0; t1[j] = 0; }
-  const uint32_t tword = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
+  uint32_t tword = 0u;
+  if constexpr (FIXED) {
+    // straight-line prologue (no branches around loads, clamped env index; invalid lanes
+    // never store): the waitcnt pass can then retire the loads one by one -- tables
+    // first, then in use order -- instead of draining everything at the first join
+    const int ic = min(i, N - 1);
+    tword = reinterpret_cast<const uint32_t*>(p.tables)[min(tid, TW - 1)];
+    episode = p.episode[ic];
+    len0 = p.ep_len[ic];
+    a = p.actions[ic];
+    agent0 = p.agent[ic];
+    goal0 = p.goal[ic];
+#pragma unroll
+    for (int j = 0; j < NDC; ++j) { dp[j] = (p.dyn_obs + (size_t)j * N)[ic]; dgi[j] = (p.dyn_goal + (size_t)j * N)[ic]; }
+#pragma unroll
+    for (int j = 0; j < NSC; ++j) so[j] = (p.static_obs + (size_t)j * N)[ic];
+    old_dist = p.prev_dist[ic];
+    total = p.total_dist[ic];
+    ret = p.ep_return[ic];
+  } else {
+  tword = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
   if (valid) {
+    // issue order = use order: vmcnt retires loads in order, so the Philox draws (keyed by
+    // episode, ep_len) and the obstacle moves start while the statics and f64s are in flight
+    if (MODE != MODE_OBSERVE) episode = p.episode[i];
+    if (MODE == MODE_STEP) {
+      len0 = p.ep_len[i];
+      if (p.actions) a = p.actions[i];
+      else if (p.deltas) { dx = p.deltas[2 * (int64_t)i]; dy = p.deltas[2 * (int64_t)i + 1]; }
+    }
     agent0 = p.agent[i];
     goal0 = p.goal[i];
     if (MODE == MODE_STEP) {
-      if (p.actions) a = p.actions[i];
-      else if (p.deltas) { dx = p.deltas[2 * (int64_t)i]; dy = p.deltas[2 * (int64_t)i + 1]; }
-      old_dist = p.prev_dist[i];
-      total = p.total_dist[i];
-      ret = p.ep_return[i];
-      len0 = p.ep_len[i];
-      // fixed slots: indices past the count re-read the last obstacle (same lines: no extra traffic)
-      if (ns0 > 0) {
-#pragma unroll
-        for (int j = 0; j < SPL; ++j) so[j] = (p.static_obs + (size_t)min(q + LPE * j, ns0 - 1) * N)[i];
-      }
       if (nd0 > 0) {
 #pragma unroll
         for (int j = 0; j < DPL; ++j) {
           const int k = min(q + LPE * j, nd0 - 1);
           dp[j] = (p.dyn_obs + (size_t)k * N)[i];
           dgi[j] = (p.dyn_goal + (size_t)k * N)[i];
-          if (p.tape) { t0[j] = (p.tape + (size_t)(2 * k) * N)[i]; t1[j] = (p.tape + (size_t)(2 * k + 1) * N)[i]; }
+          if (!FIXED && p.tape) { t0[j] = (p.tape + (size_t)(2 * k) * N)[i]; t1[j] = (p.tape + (size_t)(2 * k + 1) * N)[i]; }
         }
       }
+      // fixed slots: indices past the count re-read the last obstacle (same lines: no extra traffic)
+      if (ns0 > 0) {
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) so[j] = (p.static_obs + (size_t)min(q + LPE * j, ns0 - 1) * N)[i];
+      }
+      old_dist = p.prev_dist[i];
+      total = p.total_dist[i];
+      ret = p.ep_return[i];
     }
-    if (MODE != MODE_OBSERVE) episode = p.episode[i];
   }
-  if (tid < TW) reinterpret_cast<uint32_t*>(&t)[tid] = tword;
-  if (tid < EPB) s_slot_of[tid] = -1;
+  }
+  if (FIXED || tid < TW) reinterpret_cast<uint32_t*>(&t)[FIXED ? min(tid, TW - 1) : tid] = tword;
+  if (EPB == BLOCK_THREADS || tid < EPB) s_slot_of[tid] = -1;
   if (tid == 0) s_nreset = 0;
   __syncthreads();  // barrier 1: tables staged, all loads above have landed
   DIAG(1);
@@ -722,7 +809,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     gx = px(goal0); gy = py(goal0);
     if (MODE == MODE_STEP) {
       // ---- action -> agent move + clamp (ballenv_env.py:247-259); every lane of the group
-      if (p.actions) {
+      if (FIXED || p.actions) {
         st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
         a = a < p.num_actions ? a : 0;
         const int32_t m = t.action[a]; dx = px(m); dy = py(m);
@@ -744,41 +831,56 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       if (counter < 0) counter += p.goal_change + 1;
       if (counter > p.goal_change) counter -= p.goal_change + 1;
       const bool change = counter >= p.goal_change;
-      const bool tape = p.tape != nullptr;
-      // Philox words: obstacle k uses word k&3 of block k>>2 (both of its draws).
+      const bool tape = !FIXED && p.tape != nullptr;
+      // Philox fields: obstacle k uses 24-bit field k%5 of block k/5 (both of its draws).
       uint32_t wj[DPL];
 #pragma unroll
       for (int j = 0; j < DPL; ++j) wj[j] = 0u;
       if (!tape && !DBG(DBG_NO_PHILOX)) {
-        if constexpr (LPE == 4) {  // one block per lane (= lane parity), words swapped by DPP
-          const u4 blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(q & 1)), p.seed);
-          const uint32_t own = pick_word(blk, q), send = pick_word(blk, q ^ 1);
-          const uint32_t recv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xF, 0xF, false);
-          wj[0] = (q & 1) ? recv : own;   // k = q     : block 0, word q
-          wj[1] = (q & 1) ? own : recv;   // k = q + 4 : block 1, word q
-        } else if constexpr (LPE == 2) {  // lane q: k = q + 2j -> block j>>1, word q + 2(j&1); lane q computes block q
-          const u4 blk = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)q), p.seed);
-          const uint32_t s0 = q ? blk.x : blk.y, s1 = q ? blk.z : blk.w;   // words the partner needs
-          const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s0, 0xB1, 0xF, 0xF, false);
-          const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s1, 0xB1, 0xF, 0xF, false);
-          wj[0] = q ? r0 : blk.x;   // k = q      block 0 word q
-          wj[1] = q ? r1 : blk.z;   // k = q + 2  block 0 word q + 2
-          wj[2] = q ? blk.y : r0;   // k = q + 4  block 1 word q
-          wj[3] = q ? blk.w : r1;   // k = q + 6  block 1 word q + 2
-        } else {
-          const u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
-          wj[0] = b0.x; wj[1] = b0.y; wj[2] = b0.z; wj[3] = b0.w;
-          if (nd0 > 4) {
-            const u4 b1 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 1u), p.seed);
-            wj[4 % DPL] = b1.x; wj[5 % DPL] = b1.y; wj[6 % DPL] = b1.z; wj[7 % DPL] = b1.w;
-          }
+        const u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+        u4 b1{0u, 0u, 0u, 0u};
+        if (nd0 > 5) b1 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 1u), p.seed);
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) {
+          const int k = q + LPE * j;   // < CD = 8 <= 10: blocks 0 and 1 cover every slot
+          wj[j] = k < 5 ? pick_field(b0, k) : pick_field(b1, k - 5);
         }
       }
-      // fixed slot loops: slots past the obstacle count hold a far-away sentinel, so the
+      // FIXED: exact trip counts; one (dx, dy) per obstacle feeds both the collision test and
+      // the window-box test (the box is a superset of the cells' R-neighbourhood; the
+      // rasteriser is exact, so a box hit that lights nothing costs only raster work)
+      const int bxo = p.speed_x * (p.window / 2) + g.R, byo = p.speed_y * (p.window / 2) + g.R;
+      const uint32_t bw = nb.bw, bh = nb.bh;   // = NearBox's test, relative to the agent
+      auto obstacle = [&](int ox, int oy, bool& hit) {
+        const int dx = ox - ax, dy = oy - ay;
+        hit |= (uint32_t)__mul24(dx, dx) + (uint32_t)__mul24(dy, dy) <= R2;
+        // unconditional LDS write, predicated count: no divergent region per obstacle
+        nl.base[nl.cnt * BLOCK_THREADS] = (uint32_t)((dx + bxo - g.R) & 0xFFFF) | ((uint32_t)(dy + byo - g.R) << 16);
+        nl.cnt += ((uint32_t)(dx + bxo) <= bw && (uint32_t)(dy + byo) <= bh) ? 1 : 0;
+      };
+      if constexpr (FIXED) {
+        DIAG(7);
+        int ngs[NDC];
+#pragma unroll
+        for (int j = 0; j < NDC; ++j) {
+          int ox = px(dp[j]), oy = py(dp[j]);
+          ngs[j] = dyn_move_philox(p, t, ox, oy, dgi[j], t.speed[j], change, wj[j], st_flags);
+          if (valid) (p.dyn_obs + (size_t)j * N)[i] = pk(ox, oy);
+          obstacle(ox, oy, hd);
+        }
+        if (valid && change) {   // every obstacle re-picks its goal on the same step
+#pragma unroll
+          for (int j = 0; j < NDC; ++j) (p.dyn_goal + (size_t)j * N)[i] = (uint8_t)ngs[j];
+        }
+        DIAG(11);
+#pragma unroll
+        for (int j = 0; j < NSC; ++j) obstacle(px(so[j]), py(so[j]), hs);
+      }
+      // generic slot loops: slots past the obstacle count hold a far-away sentinel, so the
       // collision / window tests are branch-free; only their stores are skipped
       constexpr int FAR = -30000;
 #pragma unroll
-      for (int j = 0; j < DPL; ++j) {
+      for (int j = 0; j < (FIXED ? 0 : DPL); ++j) {
         const int k = q + LPE * j;
         const bool real = k < nd0;
         int ox = real ? px(dp[j]) : FAR, oy = real ? py(dp[j]) : FAR;
@@ -791,14 +893,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         int f, e;
         nl.push_if(nb.maybe(ox, oy) && g.near(ox, oy, f, e) && !DBG(DBG_NO_NEAR), f, e);
       }
-      for (int kb = CD + q; kb < Nd; kb += LPE) {  // configs with more than CD dynamic obstacles
+      for (int kb = CD + q; !FIXED && kb < Nd; kb += LPE) {  // configs with more than CD dynamic obstacles
         int32_t* pos = p.dyn_obs + (size_t)kb * N + i;
         uint8_t* gp = p.dyn_goal + (size_t)kb * N + i;
         int ox = px(*pos), oy = py(*pos);
         const int gi = *gp;
-        const u4 blk = tape ? u4{0, 0, 0, 0} : philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(kb >> 2)), p.seed);
+        const u4 blk = tape ? u4{0, 0, 0, 0} : philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, (uint32_t)(kb / 5)), p.seed);
         const int tt0 = tape ? (p.tape + (size_t)(2 * kb) * N)[i] : 0, tt1 = tape ? (p.tape + (size_t)(2 * kb + 1) * N)[i] : 0;
-        const int ng = dyn_move(p, t, ox, oy, gi, t.speed[kb], change, tape, tt0, tt1, pick_word(blk, kb & 3), st_flags);
+        const int ng = dyn_move(p, t, ox, oy, gi, t.speed[kb], change, tape, tt0, tt1, pick_field(blk, kb % 5), st_flags);
         *pos = pk(ox, oy);
         if (ng != gi) *gp = (uint8_t)ng;
         hd |= collides(ox, oy, ax, ay, R2);
@@ -808,7 +910,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       DIAG(9);
       // ---- static obstacles: collision + near test
 #pragma unroll
-      for (int j = 0; j < SPL; ++j) {
+      for (int j = 0; j < (FIXED ? 0 : SPL); ++j) {
         const int k = q + LPE * j;
         const bool real = k < ns0;
         const int ox = real ? px(so[j]) : FAR, oy = real ? py(so[j]) : FAR;
@@ -816,7 +918,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         int f, e;
         nl.push_if(nb.maybe(ox, oy) && g.near(ox, oy, f, e) && !DBG(DBG_NO_NEAR), f, e);
       }
-      for (int kb = CS + q; kb < Ns; kb += LPE) {
+      for (int kb = CS + q; !FIXED && kb < Ns; kb += LPE) {
         const int32_t o = (p.static_obs + (size_t)kb * N)[i];
         const int ox = px(o), oy = py(o);
         hs |= collides(ox, oy, ax, ay, R2);
@@ -883,7 +985,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const int quad = quadrant(ax, ay, gx, gy);
       if constexpr (WT > 0) {
         uint32_t rows[Geo<WT>::K], flat[Geo<WT>::NW];
-        raster_rows<WT, BLOCK_THREADS>(nl, g, rows);
+        raster_rows<WT, BLOCK_THREADS, FIXED>(nl, g, rows, t.hw);
 #pragma unroll
         for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k]);
         flatten<WT>(rows, flat);
@@ -935,7 +1037,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const Win g(p, ax, ay);
       uint32_t rows[Geo<WT>::K];
       if (DBG(DBG_NO_RASTER)) nl.cnt = 0;
-      raster_rows<WT, BLOCK_THREADS>(nl, g, rows);
+      raster_rows<WT, BLOCK_THREADS, FIXED>(nl, g, rows, t.hw);
 #pragma unroll
       for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k]);
       flatten<WT>(rows, flat);
@@ -1117,11 +1219,20 @@ KFn kernel_for(int mode) {
 
 struct Launch { KFn fn; int epb; int lds; };
 
-Launch pick_kernel(const be_config& c, int mode) {
-  const int W = c.window, F = 4 + W * W, nobs = c.num_static + c.num_dynamic;
+// Fixed-shape step kernels for the reference's default obstacle counts (ball_cnn_ac3.py:40-41).
+constexpr int FIX_NS = 13, FIX_ND = 5;
+
+Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false) {
+  int W = c.window;
+  const int F = 4 + W * W, nobs = c.num_static + c.num_dynamic;
   Launch L{nullptr, 0, 0};
   bool staged = true;
+  const bool fixed = fixed_ok && mode == MODE_STEP && c.num_static == FIX_NS && c.num_dynamic == FIX_ND &&
+                     c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
+  if (fixed && W == 10) { L.fn = be_kernel<10, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
+  else if (fixed && W == 5) { L.fn = be_kernel<5, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
   switch (W) {
+    case -1: break;
 #define BE_CASE(n) case n: L.fn = kernel_for<n>(mode); L.epb = envs_per_block(n); break;
     BE_CASE(1) BE_CASE(2) BE_CASE(3) BE_CASE(4) BE_CASE(5) BE_CASE(6) BE_CASE(7) BE_CASE(8)
     BE_CASE(9) BE_CASE(10) BE_CASE(11) BE_CASE(12) BE_CASE(13) BE_CASE(14) BE_CASE(15) BE_CASE(16)
@@ -1129,7 +1240,7 @@ Launch pick_kernel(const be_config& c, int mode) {
 #undef BE_CASE
     default: L.fn = kernel_for<0>(mode); L.epb = envs_per_block(0); staged = false; break;
   }
-  const int near_bytes = nobs * BLOCK_THREADS * 4;
+  const int near_bytes = (nobs + 1) * BLOCK_THREADS * 4;   // +1: predicated pushes write one slot ahead
   const int stage_bytes = staged ? L.epb * F : 0;
   L.lds = (near_bytes + stage_bytes + 15) & ~15;
   if (L.lds == 0) L.lds = 16;
@@ -1146,6 +1257,7 @@ struct be_ctx {
   int device;
   int* status;
   Tables* d_tables;
+  bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
   char err[512];
 };
 
@@ -1284,6 +1396,7 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   b.min_spawn_dist = cfg->min_spawn_dist; b.seed = cfg->seed;
   b.inv_g1 = 1.0 / ((double)cfg->goal_change_step + 1.0);
   if (const char* d = getenv("BALLENV_DEBUG_SKIP")) b.dbg = (int32_t)strtoul(d, nullptr, 0);
+  if (const char* g = getenv("BALLENV_GENERIC_KERNELS")) ctx->generic_only = atoi(g) != 0;
   Tables& t = ctx->tables;
   memset(&t, 0, sizeof t);
   for (int k = 0; k < cfg->num_dynamic; ++k) t.speed[k] = cfg->obstacle_speed[k];
@@ -1300,6 +1413,12 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
     for (int q = 0; q < cfg->num_goals; ++q)
       if (cfg->goals[q][0] != cfg->goals[g][0] || cfg->goals[q][1] != cfg->goals[g][1]) t.other[g][n++] = (uint8_t)q;
     t.n_other[g] = (uint8_t)n;
+  }
+  const int R = cfg->radius_obstacle + cfg->radius_agent;
+  for (int d = 0; d <= R && d <= HW_MAX; ++d) {   // exact integer sqrt
+    int h = 0;
+    while ((h + 1) * (h + 1) <= R * R - d * d) ++h;
+    t.hw[d] = (uint8_t)h;
   }
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipMalloc(&ctx->status, sizeof(int));
@@ -1353,12 +1472,13 @@ static KParams make_params(be_ctx* ctx, const be_state* st, const be_out* out) {
 }
 
 static int launch(be_ctx* ctx, int mode, KParams& a, void* stream) {
+  const bool fixed_ok = mode == MODE_STEP && a.tape == nullptr && a.actions != nullptr && !ctx->generic_only;
   if (((uintptr_t)a.obs & 15) || ((uintptr_t)a.obs_f32 & 15))
     return fail(ctx, BE_E_INVALID, "%s", "obs / obs_f32 must be 16-byte aligned");
   int cur = -1;
   HIP_TRY(ctx, hipGetDevice(&cur));
   if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const Launch L = pick_kernel(ctx->cfg, mode);
+  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
   hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);

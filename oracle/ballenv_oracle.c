@@ -41,9 +41,10 @@
 #define PHILOX_W1 0xBB67AE85u
 
 /* counter = (global env id, c1, c2, purpose << 24 | sub):
- *   obstacle moves  c1 = episode, c2 = ep_len before the step: obstacle k uses word k & 3
- *                   of block sub = k >> 2; its draws are randint(n0) = hi32(w*n0), then
- *                   randint(n1) = hi32(lo32(w*n0)*n1)
+ *   obstacle moves  c1 = episode, c2 = ep_len before the step: obstacle k uses the 24-bit
+ *                   field f = bits [24j, 24j+24) of block sub = k / 5 (j = k % 5, the block
+ *                   read as x | y<<32 | z<<64 | w<<96); its draws are randint(n0) = (f*n0)>>24,
+ *                   then randint(n1) = (((f*n0) mod 2^24)*n1)>>24  (n0, n1 <= 128)
  *   sampled action  c1 = episode, c2 = ep_len before the step, sub = 0
  *   reset (Philox)  c1 = the new episode number, c2 = 0, one block per quantity:
  *                   sub = 0: gx, gy, ax, ay | sub = 1 + r: agent re-sample r (ax, ay)
@@ -74,6 +75,17 @@ static uint32_t philox_word(uint64_t seed, uint32_t gid, uint32_t c1, uint32_t c
   uint32_t out[4];
   philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), out);
   return out[w & 3];
+}
+
+/* 24-bit field j (0..4) of the Philox block for (env gid, c1, c2, purpose, sub) */
+static uint32_t philox_field(uint64_t seed, uint32_t gid, uint32_t c1, uint32_t c2, uint32_t purpose,
+                             uint32_t sub, int j) {
+  uint32_t ctr[4] = {gid, c1, c2, (purpose << 24) | (sub & 0xFFFFFFu)};
+  uint32_t o[4];
+  philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), o);
+  const int bit = 24 * j, w = bit >> 5, sh = bit & 31;
+  uint64_t two = (uint64_t)o[w] | (w < 3 ? (uint64_t)o[w + 1] << 32 : 0);
+  return (uint32_t)(two >> sh) & 0xFFFFFFu;
 }
 
 /* uniform integer in [lo, hi) from one 32-bit word (multiply-shift) */
@@ -108,7 +120,7 @@ static int check_overlap_rect(const be_config* c, int32_t x1, int32_t y1, int32_
 typedef struct {
   const be_config* c;
   const int16_t* tape; int32_t tape_len; int32_t n; int32_t env; int32_t cursor;
-  int32_t word_mode; uint32_t frac;   /* step draws: successive multiply-shifts of one word */
+  int32_t word_mode; uint32_t frac;   /* step draws: successive multiply-shifts of one 24-bit field */
   uint64_t seed; uint32_t gid; uint32_t c1, c2; uint32_t purpose;
   int32_t* status;
 } draw_src;
@@ -117,9 +129,9 @@ typedef struct {
 static int32_t draw(draw_src* s, int32_t lo, int32_t hi) {
   int32_t k = s->cursor++;
   if (s->word_mode) {
-    uint64_t prod = (uint64_t)s->frac * (uint64_t)(uint32_t)(hi - lo);
-    s->frac = (uint32_t)prod;
-    return lo + (int32_t)(prod >> 32);
+    uint32_t prod = s->frac * (uint32_t)(hi - lo);   /* < 2^31 for hi - lo <= 128 */
+    s->frac = prod & 0xFFFFFFu;
+    return lo + (int32_t)(prod >> 24);
   }
   if (s->tape) {
     if (k >= s->tape_len) { *s->status |= BE_STATUS_RESET_TAPE_EXHAUSTED; return lo; }
@@ -351,9 +363,9 @@ int orc_step(const be_config* c, const be_state* st, const uint8_t* actions,
     int32_t counter = st->ep_len[i] % (c->goal_change_step + 1);
     for (int32_t k = 0; k < c->num_dynamic; ++k) {
       /* tape: rows (k*2 + d, N) of this step's (Nd, 2, N) tape.
-       * Philox: both draws from word k&3 of block k>>2 (successive multiply-shifts). */
+       * Philox: both draws from 24-bit field k%5 of block k/5 (successive multiply-shifts). */
       draw_src ds = {c, tape ? tape + (int64_t)k * 2 * N : NULL, 2, N, i, 0, tape ? 0 : 1,
-                     tape ? 0u : philox_word(c->seed, gid, episode, len0, PURPOSE_STEP_OBS, (uint32_t)k >> 2, k & 3),
+                     tape ? 0u : philox_field(c->seed, gid, episode, len0, PURPOSE_STEP_OBS, (uint32_t)k / 5, k % 5),
                      c->seed, gid, episode, len0, PURPOSE_STEP_OBS, status};
       move_obstacle(c, st, i, k, counter, &ds);
     }

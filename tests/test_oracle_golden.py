@@ -130,3 +130,38 @@ def test_philox_mode_distributions():
     a = oracle.sample_actions(cfg, 64, 7)
     counts = np.bincount(a.ravel(), minlength=9)
     assert counts.min() > 0.9 * a.size / 9 and counts.max() < 1.1 * a.size / 9
+
+
+def test_philox_mode_obstacle_moves():
+    """Perf-mode obstacle moves follow move_obstacles' distribution (ballenv_env.py:323-353):
+    with tx, ty != 0 the move is (sign tx, sign ty) w.p. 0.6 + 0.4 * P(OBS_MOVES draw = it),
+    where OBS_MOVES holds (-1,-1) twice and (1,1), (1,-1), (-1,1) once (Q4)."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg = EnvConfig(time_limit=0).to_abi(8192, 5, seed=99)
+    st = oracle.new_state(cfg)
+    out = oracle.new_out(cfg)
+    oracle.reset(cfg, st, out)
+    goals = np.array([(cfg.goals[g][0], cfg.goals[g][1]) for g in range(cfg.num_goals)])
+    hits = {1: [0, 0], 2: [0, 0]}          # weight of the directed move in OBS_MOVES -> [agree, total]
+    for t in range(40):
+        before = st["dyn_obs"].astype(int).copy()
+        gidx = st["dyn_goal"].astype(int).copy()
+        moving = (st["ep_len"] % (cfg.goal_change_step + 1)) != cfg.goal_change_step
+        actions = np.full(cfg.num_envs, 5, np.uint8)        # (0, 0): keep the agent still
+        oracle.step(cfg, st, out, actions=actions)
+        after = st["dyn_obs"].astype(int)
+        alive = out["done"] == 0
+        tx = goals[gidx][..., 0] - before[..., 0]
+        ty = goals[gidx][..., 1] - before[..., 1]
+        sel = (tx != 0) & (ty != 0) & moving[None] & alive[None]
+        mv = after - before
+        agree = (mv[..., 0] == np.sign(tx)) & (mv[..., 1] == np.sign(ty))
+        w = np.where((np.sign(tx) < 0) & (np.sign(ty) < 0), 2, 1)
+        for k in (1, 2):
+            m = sel & (w == k)
+            hits[k][0] += int(agree[m].sum())
+            hits[k][1] += int(m.sum())
+    for k, (a, n) in hits.items():
+        p = 0.6 + 0.4 * k / 9
+        assert n > 5000
+        assert abs(a / n - p) < 4 * np.sqrt(p * (1 - p) / n), (k, a / n, p)

@@ -1,10 +1,14 @@
 #!/bin/bash
 # rocprofv3 kernel-trace medians for each tools/mb_* variant binary given as args
+# (an arg "bin@VAR=value" runs tools/bin with that environment variable set)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/mbv; export TMPDIR=/tmp
-for b in "$@"; do
-  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/mbv/$b -o run -- ./tools/$b 0 > gpurun_out/mbv/$b.log 2>&1
+for spec in "$@"; do
+  bin=${spec%%@*}; b=${spec//[@=]/_}
+  if [ "$bin" != "$spec" ]; then export "${spec#*@}"; fi
+  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/mbv/$b -o run -- ./tools/$bin 0 > gpurun_out/mbv/$b.log 2>&1
+  if [ "$bin" != "$spec" ]; then v=${spec#*@}; unset "${v%%=*}"; fi
   rc=$?; echo "== $b rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/mbv/$b.log; exit $rc; }
   python3 - "$b" <<'PY'
 import csv, sys, statistics, collections

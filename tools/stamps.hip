@@ -59,6 +59,18 @@ int main(int argc, char** argv) {
     const char* sn[4] = {"  physics: action+move", "  physics: dynamic obs", "  physics: static obs", "  physics: reward+stores"};
     for (int p = 0; p < 4; ++p)
       printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", sn[p], pct(sub[p], .5), pct(sub[p], .9), pct(sub[p], .99), pct(sub[p], 1));
+    // fixed-shape kernels: 8 -> 7 Philox, 7 -> 11 dynamic moves + their tests, 11 -> 9 static tests
+    std::vector<std::vector<double>> fx(3);
+    for (int w = 0; w < DW; ++w) {
+      if (!rt[w * DP + 0] || !cy[w * DP + 7] || !cy[w * DP + 11]) continue;
+      fx[0].push_back((double)(cy[w * DP + 7] - cy[w * DP + 8]));
+      fx[1].push_back((double)(cy[w * DP + 11] - cy[w * DP + 7]));
+      fx[2].push_back((double)(cy[w * DP + 9] - cy[w * DP + 11]));
+    }
+    const char* fn[3] = {"    fixed: counter+philox", "    fixed: dyn moves", "    fixed: static tests"};
+    for (int p = 0; p < 3; ++p)
+      if (!fx[p].empty())
+        printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", fn[p], pct(fx[p], .5), pct(fx[p], .9), pct(fx[p], .99), pct(fx[p], 1));
   }
   return 0;
 }
