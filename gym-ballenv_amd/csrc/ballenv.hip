@@ -94,6 +94,7 @@ struct KParams {
   // line 5 (cold)
   double* stats;               // (slots, 8): one slot per block of the step kernel (be_stats_slots)
   int32_t reset_tape_len;
+  int32_t min_spawn_d2;        // integer d2: sqrt(d2) < min_spawn_dist  <=>  d2 < min_spawn_d2
 };
 
 // Diagnostic phase-skip bits (timing ablations only; outputs are wrong when set).  Only
@@ -109,11 +110,15 @@ enum : uint32_t { DBG_NO_STATS = 1, DBG_NO_RASTER = 2, DBG_NO_OBS = 4, DBG_NO_PH
 
 // Diagnostics-only build (-DBE_DIAG_STAMPS): per-wave phase stamps for tools/microbench.
 #ifdef BE_DIAG_STAMPS
-constexpr int DIAG_WAVES = 1 << 16, DIAG_POINTS = 12;
+constexpr int DIAG_WAVES = 1 << 16, DIAG_POINTS = 16;
 __device__ unsigned long long g_diag_rt[DIAG_WAVES][DIAG_POINTS];   // s_memrealtime (100 MHz, chip-wide)
 __device__ unsigned long long g_diag_cy[DIAG_WAVES][DIAG_POINTS];   // s_memtime (shader clock)
+__device__ unsigned int g_diag_hw[DIAG_WAVES];                       // HW_ID (cu/sh/se) | XCC_ID << 28
 __device__ __forceinline__ void diag_stamp(int point) {
   const int w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
+  if (point == 0 && (threadIdx.x & 63) == 0 && w < DIAG_WAVES)
+    g_diag_hw[w] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0x0FFFFFFFu |
+                   ((unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 28);
   if ((threadIdx.x & 63) == 0 && w < DIAG_WAVES) {
     g_diag_rt[w][point] = __builtin_amdgcn_s_memrealtime();
     g_diag_cy[w][point] = __builtin_amdgcn_s_memtime();
@@ -134,6 +139,7 @@ __device__ __forceinline__ uint32_t d2u(int dx, int dy) {
   uint32_t ax = (uint32_t)abs(dx), ay = (uint32_t)abs(dy);
   return ax * ax + ay * ay;  // < 2^32 for int16 coordinates
 }
+__device__ __forceinline__ int d2i(int dx, int dy) { return dx * dx + dy * dy; }
 __device__ __forceinline__ int isqrt_small(int n) {  // floor(sqrt(n)), 0 <= n < 2^22
   int s = (int)__builtin_amdgcn_sqrtf((float)n);
   if (s * s > n) --s;
@@ -672,6 +678,91 @@ __device__ void stage_full_row(uint8_t* dst, const uint32_t (&flat)[Geo<WT>::NW]
   }
 }
 
+// Wave-cooperative autoreset (fixed-shape step kernels).  The finished envs of one wave are
+// reset one after another by the whole wave -- the goal/agent draw is computed uniformly by
+// every lane, lane k < NS+ND draws obstacle k and ORs its window rows into a per-wave LDS
+// row buffer -- so no other wave of the block waits on them (no block barrier).  Draws use
+// reset_env_philox's counter layout, so results equal the block-cooperative path's.
+template <int WT, int NSC, int NDC>
+__device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
+                            uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
+                            uint32_t (&xrows)[Geo<WT>::K], uint32_t* wrows) {
+  constexpr int K = Geo<WT>::K;
+  const int lane = (int)(threadIdx.x & 63);
+  const int N = p.n, W = p.screen_w, H = p.screen_h;
+  const int rx = t.radius_obstacle + t.radius_agent, ry2 = t.radius_obstacle + 2 * t.radius_agent;
+  for (; m; m &= m - 1) {
+    const int l = __ffsll((long long)m) - 1;
+    int il = __builtin_amdgcn_readlane(i, l);
+    uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)gid, l);
+    uint32_t ep = (uint32_t)__builtin_amdgcn_readlane((int)episode, l) + 1u;
+    // uniform, but computed in VGPRs: a scalar Philox pins SGPRs and spills (v_writelane)
+    asm volatile("" : "+v"(il), "+v"(u), "+v"(ep));
+    // goal / agent (ballenv_env.py:115-126) and this lane's obstacle, first attempt
+    // (:131-164), drawn together: neither depends on the other's result
+    const u4 b0 = philox(u, ep, 0u, tag(PURPOSE_RESET, 0), p.seed);
+    const bool is_obs = lane < NSC + NDC, is_static = lane < NSC;
+    const uint32_t sub0 = is_static ? ((1u << 22) | ((uint32_t)lane << 12)) : ((2u << 22) | ((uint32_t)(lane - NSC) << 12));
+    u4 bo = philox(u, ep, 0u, tag(PURPOSE_RESET, sub0), p.seed);
+    const int rgx = map_range(b0.x, W - t.strip_goal_x, W), rgy = map_range(b0.y, H - t.strip_goal_y, H);
+    int rax = map_range(b0.z, 0, t.strip_agent_x), ray = map_range(b0.w, 0, t.strip_agent_y);
+    const int ax0 = rax, ay0 = ray;
+    for (int r = 0; d2i(rgx - rax, rgy - ray) < p.min_spawn_d2; ++r) {   // dist < 50  <=>  d2 < 2500 (integers)
+      if (r >= REJECT_LIMIT - 1) { if (lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+      const u4 b = philox(u, ep, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
+      rax = map_range(b.x, 0, t.strip_agent_x); ray = map_range(b.y, 0, t.strip_agent_y);
+    }
+    if (lane < K) wrows[lane] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (is_obs) {   // obstacle `lane`
+      int ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
+      int oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
+      if (is_static) {        // rejection vs the agent / goal rectangles (:145, :193-197)
+        for (int a = 1;; ++a) {
+          const bool ra = abs(ox - rax) < rx && 2 * abs(oy - ray) < ry2;
+          const bool rg = abs(ox - rgx) < rx && 2 * abs(oy - rgy) < ry2;
+          if (!ra && !rg) break;
+          if (a >= REJECT_LIMIT) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+          bo = philox(u, ep, 0u, tag(PURPOSE_RESET, sub0 | (uint32_t)a), p.seed);
+          ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
+          oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
+        }
+        (p.static_obs + (size_t)lane * N)[il] = pk(ox, oy);
+      } else {
+        const int kd = lane - NSC;
+        (p.dyn_obs + (size_t)kd * N)[il] = pk(ox, oy);
+        (p.dyn_goal + (size_t)kd * N)[il] = (uint8_t)kd;
+      }
+      const int f = ox - (rax - WT / 2), e = oy - (ray - WT / 2);   // unit cell step (fixed-shape kernels)
+      if ((uint32_t)(f + rx) <= (uint32_t)(WT - 1 + 2 * rx) && (uint32_t)(e + rx) <= (uint32_t)(K - 1 + 2 * rx)) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int ady = abs(e - k);
+          const int hw = t.hw[min(ady, HW_MAX)];
+          const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
+          if (ady <= rx && lo <= hi) atomicOr(&wrows[k], (2u << hi) - (1u << lo));
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == l) {
+      p.agent[il] = pk(rax, ray);
+      p.goal[il] = pk(rgx, rgy);
+      p.prev_dist[il] = calc_dist(rgx, rgy, ax0, ay0);   // pre-resample distance (Q9)
+      p.total_dist[il] = calc_dist(rax, ray, rgx, rgy);
+      p.ep_return[il] = 0.0;
+      p.ep_len[il] = 0;
+      p.episode[il] = ep;
+      ax = rax; ay = ray; gx = rgx; gy = rgy; ncnt = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) xrows[k] = wrows[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // ------------------------------------------------------------------ the kernel
 // MODE_STEP: physics + (autoreset) + obs.  MODE_RESET: reset masked envs + obs.
 // MODE_OBSERVE: obs only.  WT = compile-time W (0 = runtime W: no LDS staging,
@@ -1006,7 +1097,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       }
       ax = group_bcast<LPE>(ax); ay = group_bcast<LPE>(ay);
       gx = group_bcast<LPE>(gx); gy = group_bcast<LPE>(gy);
-    } else if (lead) {
+    } else if (!FIXED && lead) {
       const int slot = atomicAdd(&s_nreset, 1);   // LDS atomic: compact the block's resets
       s_slot_of[el] = (int16_t)slot;
       if (slot < RCAP) { s_reset_el[slot] = (int16_t)el; s_reset_ep[slot] = episode + 1u; }
@@ -1025,6 +1116,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       if (g.near(px(o), py(o), f, e)) nl.push(f, e);
     }
   }
+  uint32_t xrows[KR];   // window rows of a wave-reset env (fixed-shape kernels)
+#pragma unroll
+  for (int k = 0; k < KR; ++k) xrows[k] = 0u;
+  if constexpr (FIXED) {
+    const unsigned long long m = __ballot(valid && do_reset);
+    if (m) wave_resets<WT, NSC, NDC>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[tid >> 6][0]);
+  }
   DIAG(3);
 
   // ---- observation (prep_state4)
@@ -1039,7 +1137,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       if (DBG(DBG_NO_RASTER)) nl.cnt = 0;
       raster_rows<WT, BLOCK_THREADS, FIXED>(nl, g, rows, t.hw);
 #pragma unroll
-      for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k]);
+      for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k] | xrows[k]);
       flatten<WT>(rows, flat);
       quad = quadrant(ax, ay, gx, gy);
     }
@@ -1077,7 +1175,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     __syncthreads();  // barrier 2: stage written; reset list complete
 
     // 2) cooperative resets (Philox): overwrite the stage rows of the listed envs
-    if (COOP && !tape_reset) {
+    if (COOP && !FIXED && !tape_reset) {
       const int nres = s_nreset;   // block-uniform
       for (int r0 = 0; r0 < nres; r0 += RCAP) {
         const int nr = min(RCAP, nres - r0);
@@ -1117,6 +1215,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
           for (int k = 0; k < KR; ++k) s_rows[tid][k] = 0u;
         }
         __syncthreads();
+        DIAG(12);
         // phase B: every obstacle of every listed env, one per thread
         const int per = Ns + Nd;
         const int R = t.radius_obstacle + t.radius_agent;
@@ -1154,6 +1253,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
           if (g.near(ox, oy, f, e)) raster_one_lds<WT>(s_rows[s], g, f, e);
         }
         __syncthreads();
+        DIAG(13);
         // phase C: the listed envs' obs rows into the stage
         if (tid < nr) {
           uint32_t rows[Geo<WT>::K], fl[Geo<WT>::NW];
@@ -1165,6 +1265,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
           stage_full_row<WT>(stage + e_l * F, fl, quadrant(px(ag), py(ag), px(go), py(go)));
         }
         __syncthreads();
+        DIAG(14);
       }
     }
     DIAG(5);
@@ -1286,6 +1387,9 @@ int be_diag_stamps(unsigned long long* rt, unsigned long long* cy) {
   if (hipMemcpyFromSymbol(cy, HIP_SYMBOL(g_diag_cy), sizeof(g_diag_cy)) != hipSuccess) return BE_E_HIP;
   return BE_OK;
 }
+int be_diag_hwid(unsigned int* hw) {
+  return hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_diag_hw), sizeof(g_diag_hw)) == hipSuccess ? BE_OK : BE_E_HIP;
+}
 int be_diag_clear(void) {
   static unsigned long long zero[DIAG_WAVES][DIAG_POINTS];
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_rt), zero, sizeof(zero)) != hipSuccess) return BE_E_HIP;
@@ -1394,6 +1498,14 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   b.threshold_goal = cfg->threshold_goal; b.time_penalty = cfg->time_penalty;
   b.static_penalty = cfg->static_penalty; b.dynamic_penalty = cfg->dynamic_penalty;
   b.min_spawn_dist = cfg->min_spawn_dist; b.seed = cfg->seed;
+  {  // smallest integer n with sqrt(n) >= min_spawn_dist (f64, correctly rounded: monotone in n)
+    const double D = cfg->min_spawn_dist;
+    long long n = D <= 0.0 ? 0 : (long long)ceil(D * D);
+    if (n > (1ll << 30)) n = 1ll << 30;
+    while (n > 0 && sqrt((double)(n - 1)) >= D) --n;
+    while (n < (1ll << 30) && sqrt((double)n) < D) ++n;
+    b.min_spawn_d2 = (int32_t)n;
+  }
   b.inv_g1 = 1.0 / ((double)cfg->goal_change_step + 1.0);
   if (const char* d = getenv("BALLENV_DEBUG_SKIP")) b.dbg = (int32_t)strtoul(d, nullptr, 0);
   if (const char* g = getenv("BALLENV_GENERIC_KERNELS")) ctx->generic_only = atoi(g) != 0;

@@ -9,8 +9,9 @@
 #include "ballenv.h"
 extern "C" int be_diag_stamps(unsigned long long* rt, unsigned long long* cy);
 extern "C" int be_diag_clear(void);
+extern "C" int be_diag_hwid(unsigned int* hw);
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
-constexpr int DW = 1 << 16, DP = 12;
+constexpr int DW = 1 << 16, DP = 16;
 static double pct(std::vector<double> v, double p) { if (v.empty()) return 0; std::sort(v.begin(), v.end()); return v[(size_t)(p * (v.size() - 1))]; }
 int main(int argc, char** argv) {
   int N = argc > 1 ? atoi(argv[1]) : 65536;
@@ -30,8 +31,10 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   std::vector<unsigned long long> rt(DW * DP), cy(DW * DP);
   for (int rep = 0; rep < 3; ++rep) {
+    // rep 0: one cold launch after a sync; reps 1, 2: the last of 20 back-to-back launches
     be_diag_clear();
-    be_step(ctx, &st, acts + (size_t)(rep % 64) * N, nullptr, nullptr, &out, nullptr);
+    for (int k = 0; k < (rep == 0 ? 1 : 20); ++k)
+      be_step(ctx, &st, acts + (size_t)((rep * 20 + k) % 64) * N, nullptr, nullptr, &out, nullptr);
     CK(hipDeviceSynchronize());
     be_diag_stamps(rt.data(), cy.data());
     int waves = 0; unsigned long long t0 = ~0ull, t1 = 0;
@@ -43,6 +46,27 @@ int main(int argc, char** argv) {
       for (int p = 0; p < 6; ++p) ph[p].push_back((double)(cy[w * DP + p + 1] - cy[w * DP + p]));
     }
     printf("rep %d: N=%d waves=%d span(first start..last end)=%.2f us\n", rep, N, waves, (t1 - t0) * 0.01);
+    if (rep == 2) {   // where the waves ran: per XCD start spread, blocks per CU
+      std::vector<unsigned> hw(DW);
+      be_diag_hwid(hw.data());
+      std::vector<std::vector<double>> xs(16);
+      std::vector<int> per_cu(16 * 4 * 2 * 16, 0);
+      for (int w = 0; w < DW; ++w) {
+        if (!rt[w * DP + 0]) continue;
+        const unsigned h = hw[w], xcc = h >> 28, cu = (h >> 8) & 15, sh = (h >> 12) & 1, se = (h >> 13) & 3;
+        xs[xcc & 15].push_back((rt[w * DP + 0] - t0) * 0.01);
+        if ((w & 3) == 0) per_cu[(((xcc & 15) * 4 + se) * 2 + sh) * 16 + cu]++;   // one count per block (4 waves)
+      }
+      for (int x = 0; x < 16; ++x)
+        if (!xs[x].empty())
+          printf("  xcc %d: waves %zu start p0 %.2f p50 %.2f max %.2f us\n", x, xs[x].size(), pct(xs[x], 0), pct(xs[x], .5), pct(xs[x], 1));
+      std::vector<int> hist(8, 0);
+      int used = 0;
+      for (int c : per_cu) { if (c) { used++; hist[std::min(c, 7)]++; } }
+      printf("  CUs used %d; blocks per used CU histogram:", used);
+      for (int k = 1; k < 8; ++k) printf(" %d:%d", k, hist[k]);
+      printf("\n");
+    }
     printf("  wave start us: p0 %.2f p50 %.2f p90 %.2f max %.2f | wave end us: p10 %.2f p50 %.2f p90 %.2f max %.2f\n",
            pct(start, 0), pct(start, .5), pct(start, .9), pct(start, 1), pct(endt, .1), pct(endt, .5), pct(endt, .9), pct(endt, 1));
     const char* names[6] = {"entry->barrier1 (loads)", "barrier1->physics", "physics->reset list", "list->stage written", "stage->after coop reset", "coop reset->end(copy)"};
@@ -67,6 +91,19 @@ int main(int argc, char** argv) {
       fx[1].push_back((double)(cy[w * DP + 11] - cy[w * DP + 7]));
       fx[2].push_back((double)(cy[w * DP + 9] - cy[w * DP + 11]));
     }
+    // blocks that ran cooperative resets in THIS launch: 4 -> 12 phase A, 12 -> 13 phase B, 13 -> 14 phase C
+    std::vector<std::vector<double>> cr(3);
+    for (int w = 0; w < DW; ++w) {
+      const unsigned long long* r = &rt[w * DP];
+      if (!r[0] || r[12] < r[0] || r[12] > r[6] || r[14] < r[13]) continue;
+      const unsigned long long* c = &cy[w * DP];
+      cr[0].push_back((double)(c[12] - c[4])); cr[1].push_back((double)(c[13] - c[12])); cr[2].push_back((double)(c[14] - c[13]));
+    }
+    const char* cn[3] = {"    coop: barrier+phase A", "    coop: phase B", "    coop: phase C"};
+    if (!cr[0].empty()) printf("  coop-reset waves: %zu\n", cr[0].size());
+    for (int p = 0; p < 3; ++p)
+      if (!cr[p].empty())
+        printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", cn[p], pct(cr[p], .5), pct(cr[p], .9), pct(cr[p], .99), pct(cr[p], 1));
     const char* fn[3] = {"    fixed: counter+philox", "    fixed: dyn moves", "    fixed: static tests"};
     for (int p = 0; p < 3; ++p)
       if (!fx[p].empty())
