@@ -679,43 +679,63 @@ __device__ void stage_full_row(uint8_t* dst, const uint32_t (&flat)[Geo<WT>::NW]
 }
 
 // Wave-cooperative autoreset (fixed-shape step kernels).  The finished envs of one wave are
-// reset one after another by the whole wave -- the goal/agent draw is computed uniformly by
-// every lane, lane k < NS+ND draws obstacle k and ORs its window rows into a per-wave LDS
-// row buffer -- so no other wave of the block waits on them (no block barrier).  Draws use
-// reset_env_philox's counter layout, so results equal the block-cooperative path's.
+// reset by the whole wave, P = 64 / (NS+ND) envs per pass: lane s*(NS+ND) + k draws obstacle k
+// of the pass's env s (and, redundantly, that env's goal/agent) and ORs its window rows into a
+// per-wave LDS buffer, so no other wave of the block waits on them (no block barrier).  Draws
+// use reset_env_philox's counter layout, so results equal the block-cooperative path's.
+// wl: per-wave LDS scratch, >= P*(K+8) words.
 template <int WT, int NSC, int NDC>
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
-                            uint32_t (&xrows)[Geo<WT>::K], uint32_t* wrows) {
-  constexpr int K = Geo<WT>::K;
+                            uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl) {
+#ifndef BE_WAVE_RESET_ENVS
+#define BE_WAVE_RESET_ENVS 64
+#endif
+  constexpr int K = Geo<WT>::K, G = NSC + NDC, P = (64 / G < BE_WAVE_RESET_ENVS) ? 64 / G : BE_WAVE_RESET_ENVS;
+  static_assert(P >= 1, "one env's obstacles must fit a wave");
   const int lane = (int)(threadIdx.x & 63);
   const int N = p.n, W = p.screen_w, H = p.screen_h;
   const int rx = t.radius_obstacle + t.radius_agent, ry2 = t.radius_obstacle + 2 * t.radius_agent;
-  for (; m; m &= m - 1) {
-    const int l = __ffsll((long long)m) - 1;
-    int il = __builtin_amdgcn_readlane(i, l);
-    uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)gid, l);
-    uint32_t ep = (uint32_t)__builtin_amdgcn_readlane((int)episode, l) + 1u;
-    // uniform, but computed in VGPRs: a scalar Philox pins SGPRs and spills (v_writelane)
-    asm volatile("" : "+v"(il), "+v"(u), "+v"(ep));
-    // goal / agent (ballenv_env.py:115-126) and this lane's obstacle, first attempt
-    // (:131-164), drawn together: neither depends on the other's result
-    const u4 b0 = philox(u, ep, 0u, tag(PURPOSE_RESET, 0), p.seed);
-    const bool is_obs = lane < NSC + NDC, is_static = lane < NSC;
-    const uint32_t sub0 = is_static ? ((1u << 22) | ((uint32_t)lane << 12)) : ((2u << 22) | ((uint32_t)(lane - NSC) << 12));
-    u4 bo = philox(u, ep, 0u, tag(PURPOSE_RESET, sub0), p.seed);
-    const int rgx = map_range(b0.x, W - t.strip_goal_x, W), rgy = map_range(b0.y, H - t.strip_goal_y, H);
-    int rax = map_range(b0.z, 0, t.strip_agent_x), ray = map_range(b0.w, 0, t.strip_agent_y);
-    const int ax0 = rax, ay0 = ray;
-    for (int r = 0; d2i(rgx - rax, rgy - ray) < p.min_spawn_d2; ++r) {   // dist < 50  <=>  d2 < 2500 (integers)
-      if (r >= REJECT_LIMIT - 1) { if (lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
-      const u4 b = philox(u, ep, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
-      rax = map_range(b.x, 0, t.strip_agent_x); ray = map_range(b.y, 0, t.strip_agent_y);
+  const int slot = lane / G, k = lane - slot * G;
+  uint32_t* wrows = wl;            // [P][K] row masks
+  int* stash = reinterpret_cast<int*>(wl + P * K);   // [P][4]: agent xy, goal xy, pre-resample agent xy packed
+  while (m) {
+    int ls[P], n = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < P; ++s2) {   // the next (up to) P finished lanes, uniform
+      ls[s2] = m ? __ffsll((long long)m) - 1 : 0;
+      n += m ? 1 : 0;
+      m &= m - 1;
     }
-    if (lane < K) wrows[lane] = 0u;
+    // this lane's env (slot), selected from uniform per-slot readlanes
+    int il = 0; uint32_t u = 0, ep = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < P; ++s2) {
+      const int il2 = __builtin_amdgcn_readlane(i, ls[s2]);
+      const uint32_t u2 = (uint32_t)__builtin_amdgcn_readlane((int)gid, ls[s2]);
+      const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)episode, ls[s2]) + 1u;
+      il = slot == s2 ? il2 : il; u = slot == s2 ? u2 : u; ep = slot == s2 ? e2 : ep;
+    }
+    asm volatile("" : "+v"(il), "+v"(u), "+v"(ep));   // keep the Philox inputs in VGPRs
+    const bool act = slot < n;
+    if (lane < P * K) wrows[lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (is_obs) {   // obstacle `lane`
+    if (act) {
+      // goal / agent (ballenv_env.py:115-126) and obstacle k's first attempt (:131-164),
+      // drawn together: neither depends on the other's result
+      const u4 b0 = philox(u, ep, 0u, tag(PURPOSE_RESET, 0), p.seed);
+      const bool is_static = k < NSC;
+      const uint32_t sub0 = is_static ? ((1u << 22) | ((uint32_t)k << 12)) : ((2u << 22) | ((uint32_t)(k - NSC) << 12));
+      u4 bo = philox(u, ep, 0u, tag(PURPOSE_RESET, sub0), p.seed);
+      const int rgx = map_range(b0.x, W - t.strip_goal_x, W), rgy = map_range(b0.y, H - t.strip_goal_y, H);
+      int rax = map_range(b0.z, 0, t.strip_agent_x), ray = map_range(b0.w, 0, t.strip_agent_y);
+      const int ax0 = rax, ay0 = ray;
+      for (int r = 0; d2i(rgx - rax, rgy - ray) < p.min_spawn_d2; ++r) {   // dist < 50 <=> d2 < 2500 (integers)
+        if (r >= REJECT_LIMIT - 1) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+        const u4 b = philox(u, ep, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
+        rax = map_range(b.x, 0, t.strip_agent_x); ray = map_range(b.y, 0, t.strip_agent_y);
+      }
       int ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
       int oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
       if (is_static) {        // rejection vs the agent / goal rectangles (:145, :193-197)
@@ -728,36 +748,43 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
           ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
           oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
         }
-        (p.static_obs + (size_t)lane * N)[il] = pk(ox, oy);
+        (p.static_obs + (size_t)k * N)[il] = pk(ox, oy);
       } else {
-        const int kd = lane - NSC;
-        (p.dyn_obs + (size_t)kd * N)[il] = pk(ox, oy);
-        (p.dyn_goal + (size_t)kd * N)[il] = (uint8_t)kd;
+        (p.dyn_obs + (size_t)(k - NSC) * N)[il] = pk(ox, oy);
+        (p.dyn_goal + (size_t)(k - NSC) * N)[il] = (uint8_t)(k - NSC);
+      }
+      if (k == 0) {
+        stash[slot * 4 + 0] = pk(rax, ray); stash[slot * 4 + 1] = pk(rgx, rgy); stash[slot * 4 + 2] = pk(ax0, ay0);
       }
       const int f = ox - (rax - WT / 2), e = oy - (ray - WT / 2);   // unit cell step (fixed-shape kernels)
       if ((uint32_t)(f + rx) <= (uint32_t)(WT - 1 + 2 * rx) && (uint32_t)(e + rx) <= (uint32_t)(K - 1 + 2 * rx)) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const int ady = abs(e - k);
+        for (int r = 0; r < K; ++r) {
+          const int ady = abs(e - r);
           const int hw = t.hw[min(ady, HW_MAX)];
           const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
-          if (ady <= rx && lo <= hi) atomicOr(&wrows[k], (2u << hi) - (1u << lo));
+          if (ady <= rx && lo <= hi) atomicOr(&wrows[slot * K + r], (2u << hi) - (1u << lo));
         }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (lane == l) {
-      p.agent[il] = pk(rax, ray);
-      p.goal[il] = pk(rgx, rgy);
-      p.prev_dist[il] = calc_dist(rgx, rgy, ax0, ay0);   // pre-resample distance (Q9)
-      p.total_dist[il] = calc_dist(rax, ray, rgx, rgy);
-      p.ep_return[il] = 0.0;
-      p.ep_len[il] = 0;
-      p.episode[il] = ep;
-      ax = rax; ay = ray; gx = rgx; gy = rgy; ncnt = 0;
+    int own = -1;   // the slot whose env this lane owns
 #pragma unroll
-      for (int k = 0; k < K; ++k) xrows[k] = wrows[k];
+    for (int s2 = 0; s2 < P; ++s2) own = (s2 < n && lane == ls[s2]) ? s2 : own;
+    if (own >= 0) {
+      const int32_t ag = stash[own * 4 + 0], go = stash[own * 4 + 1], a0 = stash[own * 4 + 2];
+      ax = px(ag); ay = py(ag); gx = px(go); gy = py(go);
+      p.agent[i] = ag;
+      p.goal[i] = go;
+      p.prev_dist[i] = calc_dist(gx, gy, px(a0), py(a0));   // pre-resample distance (Q9)
+      p.total_dist[i] = calc_dist(ax, ay, gx, gy);
+      p.ep_return[i] = 0.0;
+      p.ep_len[i] = 0;
+      p.episode[i] = episode + 1u;
+      ncnt = 0;
+#pragma unroll
+      for (int r = 0; r < K; ++r) xrows[r] = wrows[own * K + r];
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -1121,7 +1148,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   for (int k = 0; k < KR; ++k) xrows[k] = 0u;
   if constexpr (FIXED) {
     const unsigned long long m = __ballot(valid && do_reset);
-    if (m) wave_resets<WT, NSC, NDC>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[tid >> 6][0]);
+    static_assert(!FIXED || (RCAP >= (BLOCK_THREADS / 64) * 16 && 16 * KR >= (64 / (NSC + NDC + !FIXED)) * (KR + 4)), "wave reset scratch");
+    if (m) wave_resets<WT, NSC, NDC>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0]);
   }
   DIAG(3);
 

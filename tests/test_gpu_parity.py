@@ -185,10 +185,13 @@ def test_vs_oracle_random_tape(gpu, W):
     env.close()
 
 
-@pytest.mark.parametrize("W,N", [(10, 65536), (5, 4096), (10, 1000), (7, 333)])
-def test_vs_oracle_philox_autoreset(gpu, W, N):
-    """Perf mode (Philox draws, sampled actions, in-kernel autoreset + time limit) is
-    bit-exact against the oracle run with the same counters, incl. terminal obs."""
+@pytest.mark.parametrize("W,N,given", [(10, 65536, False), (5, 4096, False), (10, 1000, False), (7, 333, False),
+                                       (10, 65536, True), (5, 4096, True), (10, 1000, True), (7, 333, True)])
+def test_vs_oracle_philox_autoreset(gpu, W, N, given):
+    """Perf mode (Philox draws, in-kernel autoreset + time limit) is bit-exact against the
+    oracle run with the same counters, incl. terminal obs.  given=False: in-kernel sampled
+    actions (generic kernel); given=True: caller actions (the fixed-shape 13+5 kernel at
+    W 5 / 10, with the wave-cooperative resets)."""
     from gym_ballenv_amd.config import EnvConfig
     cfg_py = EnvConfig(autoreset=True, time_limit=37)
     cfg = cfg_py.to_abi(N, W, seed=77)
@@ -199,11 +202,16 @@ def test_vs_oracle_philox_autoreset(gpu, W, N):
     np.testing.assert_array_equal(env.reset().cpu().numpy(), out["obs"])
     assert_state_equal(env, st, "reset")
     steps = 60 if N <= 4096 else 12
+    acts = env.sample_actions(steps, seed=5) if given else None
     for t in range(steps):
         out["terminal_obs"][:] = 0
         env.terminal_obs.zero_()
-        oracle.step(cfg, st, out)
-        obs, reward, done, info = env.step()
+        if given:
+            oracle.step(cfg, st, out, actions=acts[t].cpu().numpy())
+            obs, reward, done, info = env.step(acts[t])
+        else:
+            oracle.step(cfg, st, out)
+            obs, reward, done, info = env.step()
         d = done.cpu().numpy()
         np.testing.assert_array_equal(reward.cpu().numpy(), out["reward"], err_msg=f"t={t}")
         np.testing.assert_array_equal(d, out["done"].astype(bool), err_msg=f"t={t}")
@@ -219,6 +227,36 @@ def test_vs_oracle_philox_autoreset(gpu, W, N):
     np.testing.assert_allclose(s_gpu[1:3], s_orc[1:3], rtol=1e-12, atol=1e-9)
     env.status()
     env.close()
+
+
+@pytest.mark.parametrize("W", [10, 5])
+def test_fixed_vs_generic_kernel(gpu, W, monkeypatch):
+    """The fixed-shape step kernel (13+5 obstacles, caller actions) equals the generic one bit
+    for bit, through mass truncation (every lane of every wave resets on the same step) and the
+    reward/done/terminal outputs; BALLENV_GENERIC_KERNELS=1 forces the generic kernel."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig(time_limit=20)
+    N = 20000
+    envs = []
+    for generic in ("0", "1"):
+        monkeypatch.setenv("BALLENV_GENERIC_KERNELS", generic)
+        envs.append(make_env(cfg_py, N, W, gpu, seed=21, terminal_obs=True))
+    monkeypatch.delenv("BALLENV_GENERIC_KERNELS")
+    acts = envs[0].sample_actions(45, seed=8)
+    for e in envs:
+        e.reset()
+    for t in range(45):
+        res = [e.step(acts[t]) for e in envs]
+        for a, b in zip(res[0][:3], res[1][:3]):
+            np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=f"t={t}")
+        np.testing.assert_array_equal(res[0][3]["terminal_obs"].cpu().numpy(), res[1][3]["terminal_obs"].cpu().numpy())
+        s0, s1 = np_state(envs[0]), np_state(envs[1])
+        for k in KEYS:
+            np.testing.assert_array_equal(s0[k], s1[k], err_msg=f"t={t} {k}")
+    assert res[0][2].any()
+    for e in envs:
+        e.status()
+        e.close()
 
 
 def test_shard_invariance(gpu):
