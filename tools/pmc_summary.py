@@ -4,6 +4,7 @@ traffic = 2 * FETCH_SIZE + WRITE_SIZE  (kB -> bytes; on gfx950 FETCH_SIZE report
 bytes of wide coalesced reads: MI355X_MICROARCH.md "HBM"), averaged over the step-kernel
 dispatches of the bench's timed region (warm-up and reset dispatches skipped)."""
 import csv
+import re
 import glob
 import json
 import os
@@ -18,8 +19,9 @@ steps = int(argv[argv.index("--steps") + 1])
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     f = glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True)[0]
-    rows = [r for r in csv.DictReader(open(f)) if f"be_kernel<{window}, 0>" in r["Kernel_Name"]
+    rows = [r for r in csv.DictReader(open(f)) if re.search(rf"be_kernel<{window}, 0[,>]", r["Kernel_Name"])
             and r["Counter_Name"] == c]
+    kname = rows[0]["Kernel_Name"] if rows else None
     per = {}
     for r in rows:   # one row per dispatch (summed over instances if split)
         per[int(r["Dispatch_Id"])] = per.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
@@ -29,7 +31,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gym_ballenv_amd.config import EnvConfig, step_bytes   # noqa: E402
 algo = step_bytes(EnvConfig(), window) * envs
-out = {"kernel": f"be_kernel<{window}, 0>", "envs": envs, "window": window,
+out = {"kernel": kname, "envs": envs, "window": window,
        "fetch_size_bytes_reported": vals["FETCH_SIZE"], "write_size_bytes": vals["WRITE_SIZE"],
        "hbm_bytes_per_launch": 2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"],
        "algorithmic_bytes_per_launch": algo, "dispatches": vals["FETCH_SIZE_dispatches"],
