@@ -92,7 +92,7 @@ struct KParams {
   const int16_t* deltas; const int16_t* tape; const uint8_t* mask; const int16_t* reset_tape;
   uint8_t* truncated; uint8_t* terminal_obs; double* final_return; int32_t* final_len;
   // line 5 (cold)
-  double* stats;               // (slots, 8): one slot per block of the step kernel (be_stats_slots)
+  double* stats;               // (slots, 8): one slot per wave / block of the step kernel (be_stats_slots)
   int32_t reset_tape_len;
   int32_t min_spawn_d2;        // integer d2: sqrt(d2) < min_spawn_dist  <=>  d2 < min_spawn_d2
 };
@@ -356,8 +356,7 @@ __device__ __forceinline__ void stage_row(uint8_t* stage, int tid, const uint32_
 // Copy the block's staged rows to obs (u8) and/or obs_f32 with 16-byte stores.
 template <int BLOCK>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid, int64_t row0,
-                                         uint8_t* obs, float* obs_f32) {
-  const int tid = threadIdx.x;
+                                         uint8_t* obs, float* obs_f32, int tid = (int)threadIdx.x) {
   const int bytes = nvalid * F;
   if (obs) {
     uint8_t* dst = obs + row0 * F;
@@ -1198,8 +1197,26 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         }
       }
     }
-    if (MODE == MODE_STEP && (tid & 63) == 0) s_ws[tid >> 6] = ws;
     DIAG(4);
+    if constexpr (FIXED) {
+      // each wave owns 64 contiguous obs rows: it copies them out and settles its own stats
+      // slot -- no block barrier, so a wave that ran resets delays nobody else
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int w = tid >> 6, lane = tid & 63;
+      const int e0 = blk0 + w * 64;
+      DIAG(5);
+      copy_out<64>(stage + w * 64 * F, F, max(0, min(64, N - e0)), (int64_t)e0, p.obs, p.obs_f32, lane);
+      if (p.stats && lane == 0 && ws.n > 0.0) {
+        double* slot = p.stats + ((size_t)blockIdx.x * (BLOCK_THREADS / 64) + w) * 8;
+        slot[0] += ws.n; slot[1] += ws.s1; slot[2] += ws.s2; slot[3] += ws.sl;
+        slot[4] = fmin(slot[4], ws.mn); slot[5] = fmax(slot[5], ws.mx);
+      }
+      DIAG(6);
+      return;
+    }
+    if (MODE == MODE_STEP && (tid & 63) == 0) s_ws[tid >> 6] = ws;
     __syncthreads();  // barrier 2: stage written; reset list complete
 
     // 2) cooperative resets (Philox): overwrite the stage rows of the listed envs
@@ -1503,8 +1520,9 @@ const char* be_last_error(const be_ctx* ctx) { return ctx ? ctx->err : g_err; }
 
 int64_t be_stats_slots(const be_config* c) {
   if (!c || c->num_envs < 1 || c->window < 1) return 0;
-  const Launch L = pick_kernel(*c, MODE_STEP);
-  return ((int64_t)c->num_envs + L.epb - 1) / L.epb;
+  // one slot per wave of 64 envs: the fixed-shape step kernels settle stats per wave, the
+  // generic ones per block (fewer slots, a prefix of these)
+  return ((int64_t)c->num_envs + 63) / 64;
 }
 
 int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
