@@ -95,13 +95,16 @@ struct KParams {
   double* stats;               // (slots, 8): one slot per wave / block of the step kernel (be_stats_slots)
   int32_t reset_tape_len;
   int32_t min_spawn_d2;        // integer d2: sqrt(d2) < min_spawn_dist  <=>  d2 < min_spawn_d2
+  // fixed-shape kernels only (pick_kernel checks the preconditions):
+  uint32_t amx, amy;           // action a's (dx+1, dy+1) at bits 2a..2a+1 (every move in {-1,0,1})
+  int32_t num_goals;           // goals pairwise distinct: newGoalList(g)[pick] = pick + (pick >= g)
 };
 
 // Diagnostic phase-skip bits (timing ablations only; outputs are wrong when set).  Only
 // diagnostics builds (-DBE_DIAG_STAMPS or -DBE_DIAG_SKIP) read them; in production DBG(x) is 0.
 enum : uint32_t { DBG_NO_STATS = 1, DBG_NO_RASTER = 2, DBG_NO_OBS = 4, DBG_NO_PHILOX = 8, DBG_NO_DYN = 16,
                   DBG_NO_NEAR = 32, DBG_EXIT_ENTRY = 64, DBG_EXIT_BARRIER = 128, DBG_EXIT_PHYSICS = 256,
-                  DBG_EXIT_RASTER = 512 };
+                  DBG_EXIT_RASTER = 512, DBG_WAIT_LOADS = 1024 };
 #if defined(BE_DIAG_STAMPS) || defined(BE_DIAG_SKIP)
 #define DBG(x) (p.dbg & (x))
 #else
@@ -140,6 +143,11 @@ __device__ __forceinline__ uint32_t d2u(int dx, int dy) {
   return ax * ax + ay * ay;  // < 2^32 for int16 coordinates
 }
 __device__ __forceinline__ int d2i(int dx, int dy) { return dx * dx + dy * dy; }
+// element idx of a uniform base pointer, as base + zext(32-bit byte offset)
+template <class T>
+__device__ __forceinline__ T ld_s(const T* base, uint32_t idx) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (size_t)(idx * (uint32_t)sizeof(T)));
+}
 __device__ __forceinline__ int isqrt_small(int n) {  // floor(sqrt(n)), 0 <= n < 2^22
   int s = (int)__builtin_amdgcn_sqrtf((float)n);
   if (s * s > n) --s;
@@ -149,6 +157,7 @@ __device__ __forceinline__ int isqrt_small(int n) {  // floor(sqrt(n)), 0 <= n <
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
 struct u4 { uint32_t x, y, z, w; };
+typedef short v2s __attribute__((ext_vector_type(2)));   // a packed (x, y) int16 position
 
 // Philox4x32-10 (Salmon et al., SC'11); same as oracle/ballenv_oracle.c
 __device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, unsigned long long seed) {
@@ -260,18 +269,20 @@ template <int WT> struct Geo {
   static constexpr int F = 4 + WT * WT;
 };
 
-// Rasterise the near list into K row bitmasks (compile-time W).  HWT: unit cell step and
-// R <= HW_MAX, so a row's half-width comes from the LDS table instead of an isqrt.
+// Rasterise the near list into K row bitmasks (compile-time W).  HWT (fixed-shape kernels):
+// unit cell step, R <= HW_MAX and agent-relative list entries; a row's half-width comes from
+// the LDS table instead of an isqrt.
 template <int WT, int BLOCK, bool HWT = false>
 __device__ __forceinline__ void raster_rows(const NearList<BLOCK>& nl, const Win& g, uint32_t (&rows)[Geo<WT>::K],
                                             const uint8_t* hwt = nullptr) {
   constexpr int K = Geo<WT>::K;
 #pragma unroll
   for (int k = 0; k < K; ++k) rows[k] = 0u;
-  if constexpr (HWT) {
+  if constexpr (HWT) {   // entries are agent-relative (dx, dy); unit cell step, so f = dx + W/2
     for (int n = 0; n < nl.cnt; ++n) {
       int f, e;
       nl.get(n, f, e);
+      f += WT / 2; e += WT / 2;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int ady = abs(e - k);
@@ -625,6 +636,28 @@ __device__ __forceinline__ int dyn_move_philox(const KParams& p, const Tables& t
   return (change && n_other > 0) ? ng : gi;
 }
 
+// dyn_move_philox for pairwise-distinct goals (the fixed-shape kernels): newGoalList(g) is
+// every other goal in order, so the pick needs no table; n_other = num_goals - 1 >= 1.
+__device__ __forceinline__ int dyn_move_fixed(const KParams& p, const Tables& t, int& ox, int& oy, int gi, int speed,
+                                              bool change, uint32_t f, uint32_t& flags) {
+  const int32_t gp = t.goal[gi];
+  const int tx = px(gp) - ox, ty = py(gp) - oy;
+  const bool both = (tx != 0) & (ty != 0);
+  const uint32_t p1 = __umul24(f, 100u);
+  const uint32_t src = both ? (p1 & 0xFFFFFFu) : f;
+  const uint32_t m2 = 2u * (__umul24(src, 9u) >> 24);            // 2 * OBS_MOVES index
+  const bool directed = both & ((int)(p1 >> 24) < p.certainty);
+  const int sx = (tx > 0) - (tx < 0), sy = (ty > 0) - (ty < 0);
+  const int rx = (int)((OBS_MX >> m2) & 3u) - 1, ry = (int)((OBS_MY >> m2) & 3u) - 1;
+  const int mx = directed ? sx : rx, my = directed ? sy : ry;
+  const int step = change ? 0 : speed;                             // goal change: no move (Q5)
+  const int nx = ox + mx * step, ny = oy + my * step;
+  const int pick = (int)(__umul24(f, (uint32_t)(p.num_goals - 1)) >> 24);
+  flags |= ((uint32_t)(nx + 32768) > 65535u || (uint32_t)(ny + 32768) > 65535u) ? (uint32_t)BE_STATUS_COORD_RANGE : 0u;
+  ox = nx; oy = ny;
+  return change ? pick + (pick >= gi ? 1 : 0) : gi;
+}
+
 // Window-box pre-filter: an obstacle can light a cell only if it lies in the cell box grown by R.
 struct NearBox {
   int bx0, by0; uint32_t bw, bh;
@@ -683,14 +716,11 @@ __device__ void stage_full_row(uint8_t* dst, const uint32_t (&flat)[Geo<WT>::NW]
 // per-wave LDS buffer, so no other wave of the block waits on them (no block barrier).  Draws
 // use reset_env_philox's counter layout, so results equal the block-cooperative path's.
 // wl: per-wave LDS scratch, >= P*(K+8) words.
-template <int WT, int NSC, int NDC>
+template <int WT, int NSC, int NDC, int PMAX>
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
                             uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl) {
-#ifndef BE_WAVE_RESET_ENVS
-#define BE_WAVE_RESET_ENVS 64
-#endif
-  constexpr int K = Geo<WT>::K, G = NSC + NDC, P = (64 / G < BE_WAVE_RESET_ENVS) ? 64 / G : BE_WAVE_RESET_ENVS;
+  constexpr int K = Geo<WT>::K, G = NSC + NDC, P = (64 / G < PMAX) ? 64 / G : PMAX;
   static_assert(P >= 1, "one env's obstacles must fit a wave");
   const int lane = (int)(threadIdx.x & 63);
   const int N = p.n, W = p.screen_w, H = p.screen_h;
@@ -718,7 +748,9 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
     asm volatile("" : "+v"(il), "+v"(u), "+v"(ep));   // keep the Philox inputs in VGPRs
     const bool act = slot < n;
     if (lane < P * K) wrows[lane] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // intra-wave LDS hand-offs: a wave's LDS operations execute in issue order, so only the
+    // compiler must keep them in program order (a memory fence would also drain the stores)
+    asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     if (act) {
       // goal / agent (ballenv_env.py:115-126) and obstacle k's first attempt (:131-164),
@@ -735,6 +767,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
         const u4 b = philox(u, ep, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
         rax = map_range(b.x, 0, t.strip_agent_x); ray = map_range(b.y, 0, t.strip_agent_y);
       }
+      DIAG(12);
       int ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
       int oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
       if (is_static) {        // rejection vs the agent / goal rectangles (:145, :193-197)
@@ -758,7 +791,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
       const int f = ox - (rax - WT / 2), e = oy - (ray - WT / 2);   // unit cell step (fixed-shape kernels)
       if ((uint32_t)(f + rx) <= (uint32_t)(WT - 1 + 2 * rx) && (uint32_t)(e + rx) <= (uint32_t)(K - 1 + 2 * rx)) {
 #pragma unroll
-        for (int r = 0; r < K; ++r) {
+        for (int r = 0; r < K; ++r) {   // few lanes get here: same-address LDS atomics stay cheap
           const int ady = abs(e - r);
           const int hw = t.hw[min(ady, HW_MAX)];
           const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
@@ -766,8 +799,9 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+    DIAG(13);
     int own = -1;   // the slot whose env this lane owns
 #pragma unroll
     for (int s2 = 0; s2 < P; ++s2) own = (s2 < n && lane == ls[s2]) ? s2 : own;
@@ -776,8 +810,9 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
       ax = px(ag); ay = py(ag); gx = px(go); gy = py(go);
       p.agent[i] = ag;
       p.goal[i] = go;
-      p.prev_dist[i] = calc_dist(gx, gy, px(a0), py(a0));   // pre-resample distance (Q9)
-      p.total_dist[i] = calc_dist(ax, ay, gx, gy);
+      const double td = calc_dist(ax, ay, gx, gy);
+      p.prev_dist[i] = a0 == ag ? td : calc_dist(gx, gy, px(a0), py(a0));   // pre-resample distance (Q9)
+      p.total_dist[i] = td;
       p.ep_return[i] = 0.0;
       p.ep_len[i] = 0;
       p.episode[i] = episode + 1u;
@@ -786,6 +821,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
       for (int r = 0; r < K; ++r) xrows[r] = wrows[own * K + r];
     }
     __builtin_amdgcn_wave_barrier();
+    DIAG(14);
   }
 }
 
@@ -845,6 +881,17 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   int fin_len = 0;
   uint32_t episode = 0;
   uint32_t st_flags = 0;   // BE_STATUS_* raised by this lane, published once per wave
+  // fixed-shape kernels defer the step's state / output stores to the very end of the wave
+  // (a store still in flight makes later register reuse wait for vmcnt(0), on the critical path)
+#ifndef BE_DEFER_STORES
+#define BE_DEFER_STORES 0   // measured neutral; kept as a diagnostics switch
+#endif
+  constexpr bool DEFER = FIXED && BE_DEFER_STORES;
+  constexpr int DN = FIXED ? NDC : 1;
+  int32_t dfr_dyn[DN];
+  int dfr_goal[DN];
+  bool dfr_change = false, dfr_trunc = false;
+  double dfr_reward = 0.0, dfr_dist = 0.0;
   const uint32_t gid = (uint32_t)p.gid0 + (uint32_t)i;
 
   // ---- phase 0: issue every load of this env (independent, coalesced across the wave)
@@ -864,20 +911,21 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     // straight-line prologue (no branches around loads, clamped env index; invalid lanes
     // never store): the waitcnt pass can then retire the loads one by one -- tables
     // first, then in use order -- instead of draining everything at the first join
-    const int ic = min(i, N - 1);
-    tword = reinterpret_cast<const uint32_t*>(p.tables)[min(tid, TW - 1)];
-    episode = p.episode[ic];
-    len0 = p.ep_len[ic];
-    a = p.actions[ic];
-    agent0 = p.agent[ic];
-    goal0 = p.goal[ic];
+    // (32-bit unsigned element offsets from uniform bases: global_load's SGPR-base form)
+    const uint32_t ic = (uint32_t)min(i, N - 1);
+    tword = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid, TW - 1));
+    episode = ld_s(p.episode, ic);
+    len0 = ld_s(p.ep_len, ic);
+    a = ld_s(p.actions, ic);
+    agent0 = ld_s(p.agent, ic);
+    goal0 = ld_s(p.goal, ic);
 #pragma unroll
-    for (int j = 0; j < NDC; ++j) { dp[j] = (p.dyn_obs + (size_t)j * N)[ic]; dgi[j] = (p.dyn_goal + (size_t)j * N)[ic]; }
+    for (int j = 0; j < NDC; ++j) { dp[j] = ld_s(p.dyn_obs + (size_t)j * N, ic); dgi[j] = ld_s(p.dyn_goal + (size_t)j * N, ic); }
 #pragma unroll
-    for (int j = 0; j < NSC; ++j) so[j] = (p.static_obs + (size_t)j * N)[ic];
-    old_dist = p.prev_dist[ic];
-    total = p.total_dist[ic];
-    ret = p.ep_return[ic];
+    for (int j = 0; j < NSC; ++j) so[j] = ld_s(p.static_obs + (size_t)j * N, ic);
+    old_dist = ld_s(p.prev_dist, ic);
+    total = ld_s(p.total_dist, ic);
+    ret = ld_s(p.ep_return, ic);
   } else {
   tword = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
   if (valid) {
@@ -915,8 +963,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   if (FIXED || tid < TW) reinterpret_cast<uint32_t*>(&t)[FIXED ? min(tid, TW - 1) : tid] = tword;
   if (EPB == BLOCK_THREADS || tid < EPB) s_slot_of[tid] = -1;
   if (tid == 0) s_nreset = 0;
-  __syncthreads();  // barrier 1: tables staged, all loads above have landed
+  __syncthreads();  // barrier 1: tables staged (the state loads retire in order as they are used)
   DIAG(1);
+  if (DBG(DBG_WAIT_LOADS)) {   // diagnostics: when has every load of this wave landed?
+    __builtin_amdgcn_s_waitcnt(0);   // vmcnt(0) expcnt(0) lgkmcnt(0)
+    DIAG(15);
+  }
   if (DBG(DBG_EXIT_BARRIER)) {
     if (valid && (agent0 ^ goal0 ^ so[0] ^ dp[0] ^ (int)len0 ^ (int)old_dist) == 0x7fffffff) p.obs[i] = 1;
     return;
@@ -926,7 +978,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     gx = px(goal0); gy = py(goal0);
     if (MODE == MODE_STEP) {
       // ---- action -> agent move + clamp (ballenv_env.py:247-259); every lane of the group
-      if (FIXED || p.actions) {
+      if (FIXED) {   // unit moves from the packed kernel-argument table: no LDS round trip
+        st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
+        const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
+        dx = (int)((p.amx >> sh) & 3u) - 1; dy = (int)((p.amy >> sh) & 3u) - 1;
+      } else if (p.actions) {
         st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
         a = a < p.num_actions ? a : 0;
         const int32_t m = t.action[a]; dx = px(m); dy = py(m);
@@ -975,23 +1031,41 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         nl.base[nl.cnt * BLOCK_THREADS] = (uint32_t)((dx + bxo - g.R) & 0xFFFF) | ((uint32_t)(dy + byo - g.R) << 16);
         nl.cnt += ((uint32_t)(dx + bxo) <= bw && (uint32_t)(dy + byo) <= bh) ? 1 : 0;
       };
+      // packed int16x2 form: saturating subtract (a saturated offset is out of reach either way,
+      // as is the true one), dx^2 + dy^2 by one v_dot2 (compared unsigned: no overflow case)
+      const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
+      typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+      const v2s boxo = {(short)bxo, (short)byo};
+      const v2u boxw = {(unsigned short)bw, (unsigned short)bh};
+      // near-list entries are agent-relative (dx, dy) here; the raster adds the window offset
+      auto obstacle_pk = [&](int32_t opk, bool& hit) {
+        const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
+        hit |= (uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2;
+        const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
+        const v2u over = __builtin_elementwise_sub_sat(b, boxw);   // (0, 0) iff inside the box
+        nl.base[nl.cnt * BLOCK_THREADS] = __builtin_bit_cast(uint32_t, d);
+        nl.cnt += __builtin_bit_cast(uint32_t, over) == 0u ? 1 : 0;
+      };
       if constexpr (FIXED) {
         DIAG(7);
         int ngs[NDC];
 #pragma unroll
         for (int j = 0; j < NDC; ++j) {
           int ox = px(dp[j]), oy = py(dp[j]);
-          ngs[j] = dyn_move_philox(p, t, ox, oy, dgi[j], t.speed[j], change, wj[j], st_flags);
-          if (valid) (p.dyn_obs + (size_t)j * N)[i] = pk(ox, oy);
-          obstacle(ox, oy, hd);
+          ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[j], change, wj[j], st_flags);
+          const int32_t npk = pk(ox, oy);
+          dfr_dyn[j % DN] = npk; dfr_goal[j % DN] = ngs[j];
+          if (!DEFER && valid) (p.dyn_obs + (size_t)j * N)[i] = npk;
+          obstacle_pk(npk, hd);
         }
-        if (valid && change) {   // every obstacle re-picks its goal on the same step
+        dfr_change = change;   // every obstacle re-picks its goal on the same step
+        if (!DEFER && valid && change) {
 #pragma unroll
           for (int j = 0; j < NDC; ++j) (p.dyn_goal + (size_t)j * N)[i] = (uint8_t)ngs[j];
         }
         DIAG(11);
 #pragma unroll
-        for (int j = 0; j < NSC; ++j) obstacle(px(so[j]), py(so[j]), hs);
+        for (int j = 0; j < NSC; ++j) obstacle_pk(so[j], hs);
       }
       // generic slot loops: slots past the obstacle count hold a far-away sentinel, so the
       // collision / window tests are branch-free; only their stores are skipped
@@ -1058,7 +1132,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const bool env_done = (dist < p.threshold_goal) || hs || hd;
       const bool trunc = p.time_limit > 0 && len >= p.time_limit;
       done = env_done || trunc;
-      if (lead) {
+      dfr_reward = reward; dfr_dist = dist; dfr_trunc = trunc && !env_done;
+      if (!DEFER && lead) {
         p.reward[i] = reward;
         p.done[i] = (uint8_t)done;
         if (p.truncated) p.truncated[i] = (uint8_t)(trunc && !env_done);
@@ -1148,7 +1223,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   if constexpr (FIXED) {
     const unsigned long long m = __ballot(valid && do_reset);
     static_assert(!FIXED || (RCAP >= (BLOCK_THREADS / 64) * 16 && 16 * KR >= (64 / (NSC + NDC + !FIXED)) * (KR + 4)), "wave reset scratch");
-    if (m) wave_resets<WT, NSC, NDC>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0]);
+    // one finished env (the common case): the lean single-env pass; several: up to 3 per pass
+    if (m && !(m & (m - 1)))
+      wave_resets<WT, NSC, NDC, 1>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0]);
+    else if (m)
+      wave_resets<WT, NSC, NDC, 64>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0]);
   }
   DIAG(3);
 
@@ -1173,7 +1252,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       return;
     }
     if (valid) {  // lane q writes words (bytes, when F % 4 != 0) q, q+LPE, ... of its env's row
-      if constexpr ((F & 3) == 0) {
+      auto word = [&](int w) -> uint32_t {
+        const int jc = 4 * (w - 1);  // first cell of this word (nibble aligned)
+        return w == 0 ? 1u << (8 * quad) : (((flat[jc >> 5] >> (jc & 31)) & 0xFu) * 0x00204081u) & 0x01010101u;
+      };
+      if constexpr (LPE == 1 && (F & 7) == 0) {   // 8-byte LDS stores (half the ds_write count)
+        uint2* dst = reinterpret_cast<uint2*>(stage + el * F);
+#pragma unroll
+        for (int w = 0; w < F / 8; ++w) dst[w] = make_uint2(word(2 * w), word(2 * w + 1));
+      } else if constexpr ((F & 3) == 0) {
         uint32_t* dst = reinterpret_cast<uint32_t*>(stage + el * F);
 #pragma unroll
         for (int w0 = 0; w0 < F / 4; w0 += LPE) {
@@ -1208,6 +1295,27 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const int e0 = blk0 + w * 64;
       DIAG(5);
       copy_out<64>(stage + w * 64 * F, F, max(0, min(64, N - e0)), (int64_t)e0, p.obs, p.obs_f32, lane);
+      if (DEFER && valid) {   // the deferred per-env stores (a reset env's state was written by wave_resets)
+        p.reward[i] = dfr_reward;
+        p.done[i] = (uint8_t)done;
+        if (p.truncated) p.truncated[i] = (uint8_t)dfr_trunc;
+        if (done) {
+          if (p.final_return) p.final_return[i] = fin_ret;
+          if (p.final_len) p.final_len[i] = fin_len;
+        }
+        if (!do_reset) {
+          p.agent[i] = pk(ax, ay);
+          p.prev_dist[i] = dfr_dist;
+          p.ep_return[i] = fin_ret;
+          p.ep_len[i] = fin_len;
+#pragma unroll
+          for (int j = 0; j < DN; ++j) (p.dyn_obs + (size_t)j * N)[i] = dfr_dyn[j];
+          if (dfr_change) {
+#pragma unroll
+            for (int j = 0; j < DN; ++j) (p.dyn_goal + (size_t)j * N)[i] = (uint8_t)dfr_goal[j];
+          }
+        }
+      }
       if (p.stats && lane == 0 && ws.n > 0.0) {
         double* slot = p.stats + ((size_t)blockIdx.x * (BLOCK_THREADS / 64) + w) * 8;
         slot[0] += ws.n; slot[1] += ws.s1; slot[2] += ws.s2; slot[3] += ws.sl;
@@ -1404,6 +1512,8 @@ struct be_ctx {
   int* status;
   Tables* d_tables;
   bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
+  bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
+  bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
   char err[512];
 };
 
@@ -1544,6 +1654,17 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   b.threshold_goal = cfg->threshold_goal; b.time_penalty = cfg->time_penalty;
   b.static_penalty = cfg->static_penalty; b.dynamic_penalty = cfg->dynamic_penalty;
   b.min_spawn_dist = cfg->min_spawn_dist; b.seed = cfg->seed;
+  b.num_goals = cfg->num_goals;
+  ctx->unit_moves = cfg->num_actions <= 16;
+  for (int a = 0; a < cfg->num_actions && a < 16; ++a) {
+    const int mx = cfg->actions[a][0], my = cfg->actions[a][1];
+    if (mx < -1 || mx > 1 || my < -1 || my > 1) ctx->unit_moves = false;
+    else { b.amx |= (uint32_t)(mx + 1) << (2 * a); b.amy |= (uint32_t)(my + 1) << (2 * a); }
+  }
+  ctx->distinct_goals = cfg->num_goals >= 2;
+  for (int g = 0; g < cfg->num_goals; ++g)
+    for (int h = 0; h < g; ++h)
+      if (cfg->goals[g][0] == cfg->goals[h][0] && cfg->goals[g][1] == cfg->goals[h][1]) ctx->distinct_goals = false;
   {  // smallest integer n with sqrt(n) >= min_spawn_dist (f64, correctly rounded: monotone in n)
     const double D = cfg->min_spawn_dist;
     long long n = D <= 0.0 ? 0 : (long long)ceil(D * D);
@@ -1630,7 +1751,8 @@ static KParams make_params(be_ctx* ctx, const be_state* st, const be_out* out) {
 }
 
 static int launch(be_ctx* ctx, int mode, KParams& a, void* stream) {
-  const bool fixed_ok = mode == MODE_STEP && a.tape == nullptr && a.actions != nullptr && !ctx->generic_only;
+  const bool fixed_ok = mode == MODE_STEP && a.tape == nullptr && a.actions != nullptr && !ctx->generic_only &&
+                        ctx->unit_moves && ctx->distinct_goals;
   if (((uintptr_t)a.obs & 15) || ((uintptr_t)a.obs_f32 & 15))
     return fail(ctx, BE_E_INVALID, "%s", "obs / obs_f32 must be 16-byte aligned");
   int cur = -1;

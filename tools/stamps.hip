@@ -91,19 +91,29 @@ int main(int argc, char** argv) {
       fx[1].push_back((double)(cy[w * DP + 11] - cy[w * DP + 7]));
       fx[2].push_back((double)(cy[w * DP + 9] - cy[w * DP + 11]));
     }
-    // blocks that ran cooperative resets in THIS launch: 4 -> 12 phase A, 12 -> 13 phase B, 13 -> 14 phase C
+    // waves that ran resets in THIS launch: coop (generic): 4 -> 12 phase A, 12 -> 13 B, 13 -> 14 C;
+    // wave resets (fixed-shape): 2 -> 12 draws, 12 -> 13 obstacles + raster, 13 -> 14 owner stores
     std::vector<std::vector<double>> cr(3);
     for (int w = 0; w < DW; ++w) {
       const unsigned long long* r = &rt[w * DP];
       if (!r[0] || r[12] < r[0] || r[12] > r[6] || r[14] < r[13]) continue;
       const unsigned long long* c = &cy[w * DP];
-      cr[0].push_back((double)(c[12] - c[4])); cr[1].push_back((double)(c[13] - c[12])); cr[2].push_back((double)(c[14] - c[13]));
+      cr[0].push_back((double)(c[12] - (c[12] > c[4] ? c[4] : c[2]))); cr[1].push_back((double)(c[13] - c[12])); cr[2].push_back((double)(c[14] - c[13]));
     }
     const char* cn[3] = {"    coop: barrier+phase A", "    coop: phase B", "    coop: phase C"};
     if (!cr[0].empty()) printf("  coop-reset waves: %zu\n", cr[0].size());
     for (int p = 0; p < 3; ++p)
       if (!cr[p].empty())
         printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", cn[p], pct(cr[p], .5), pct(cr[p], .9), pct(cr[p], .99), pct(cr[p], 1));
+    {   // BALLENV_DEBUG_SKIP=1024: barrier 1 -> every load landed
+      std::vector<double> la;
+      for (int w = 0; w < DW; ++w) {
+        const unsigned long long* r = &rt[w * DP];
+        if (r[0] && r[15] >= r[0] && r[15] <= r[6]) la.push_back((double)(cy[w * DP + 15] - cy[w * DP + 1]));
+      }
+      if (!la.empty())
+        printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", "  barrier1 -> loads landed", pct(la, .5), pct(la, .9), pct(la, .99), pct(la, 1));
+    }
     const char* fn[3] = {"    fixed: counter+philox", "    fixed: dyn moves", "    fixed: static tests"};
     for (int p = 0; p < 3; ++p)
       if (!fx[p].empty())
