@@ -97,7 +97,8 @@ def main():
     N, W = args.envs, args.window
     cfg = gb.EnvConfig()
     env = gb.BatchedBallEnv(N, W, cfg, device=dev, seed=0xBA11, env_offset=rank * N)
-    B = gb.step_bytes(cfg, W)
+    B = gb.survey_step_bytes(cfg, W)          # SURVEY §8(d) per-unit figure (390 B at the defaults)
+    B_eng = gb.step_bytes(cfg, W)             # what the packed layout actually moves (275 B)
     lib = _abi.lib()
     K, WU = args.steps, args.warmup
     actions = env.sample_actions(K + WU, seed=0xBA11)            # (steps, N) u8, resident in HBM
@@ -165,7 +166,8 @@ def main():
 
     total_steps = K * N * world
     value = total_steps / elapsed
-    achieved = B * N / (kern_ms * 1e-3) / 1e9                  # GB/s, algorithmic, per launch
+    achieved = B * N / (kern_ms * 1e-3) / 1e9                  # GB/s, algorithmic (§8(d)), per launch
+    achieved_eng = B_eng * N / (kern_ms * 1e-3) / 1e9          # GB/s, engine bytes, per launch
 
     # HBM-side bytes per launch from the committed PMC passes (tools/pmc_bench.sh):
     # 2 x FETCH_SIZE (gfx950 reports half of wide reads) + WRITE_SIZE, same kernel / envs / W
@@ -189,7 +191,9 @@ def main():
                        "launch": "hipGraph replay of be_step launches" if args.mode == "graph" else "eager"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_env_step": B, "kernel_us_mean": kern_ms * 1e3,
+                         "bytes_per_env_step": B, "bytes_source": "SURVEY.md 8(d): 82+8*Ns+20*Nd+4+W^2",
+                         "engine_bytes_per_env_step": B_eng, "engine_achieved": achieved_eng,
+                         "engine_frac": achieved_eng / HBM_PEAK_GBS, "kernel_us_mean": kern_ms * 1e3,
                          "kernel": f"be_kernel<{W}, 0> (MODE_STEP)", "traffic_source": traffic_src},
             "cpu_baseline": base,
             "episodes": ep,

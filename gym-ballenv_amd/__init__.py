@@ -12,7 +12,7 @@ of include/ballenv.h (libballenv.so, built in-tree).
 
     env = gb.make('gymball-v0', window=5)               # single-env gym surface
 """
-from .config import EnvConfig, MOVE_LIST, step_bytes
+from .config import EnvConfig, MOVE_LIST, step_bytes, survey_step_bytes
 from .spaces import Box, Discrete
 from ._abi import BallEnvError
 
@@ -31,5 +31,5 @@ def __getattr__(name):
     raise AttributeError(name)
 
 
-__all__ = ["EnvConfig", "MOVE_LIST", "step_bytes", "Box", "Discrete", "BallEnvError", "BatchedBallEnv",
+__all__ = ["EnvConfig", "MOVE_LIST", "step_bytes", "survey_step_bytes", "Box", "Discrete", "BallEnvError", "BatchedBallEnv",
            "BallEnv", "make", "TimeLimit", "shard", "gather_stats", "combine_stats"]

@@ -121,3 +121,14 @@ def step_bytes(cfg: EnvConfig, window: int) -> int:
     """Algorithmic HBM bytes per env-step of the step kernel."""
     return _abi.step_bytes(cfg.to_abi(1, window))
 
+
+
+def survey_step_bytes(cfg: EnvConfig, window: int) -> int:
+    """SURVEY.md §8(d)'s algorithmic bytes per env-step (the roofline's per-unit figure).
+
+    It prices the step-API traffic of the reference's natural SoA layout:
+    int32 coordinates, a stored per-obstacle counter and a u8 obs,
+    ``82 + 8*Ns + 20*Nd + (4 + W^2)`` = 390 B at Ns=13, Nd=5, W=10.
+    ``step_bytes`` is what this engine's packed layout actually moves (275 B there).
+    """
+    return 82 + 8 * cfg.num_static + 20 * cfg.num_dynamic + 4 + window * window
