@@ -51,6 +51,10 @@ def parse():
     p.add_argument("--cpu-procs", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph-chunk", type=int, default=250, help="steps per captured graph")
+    p.add_argument("--policy-steps", type=int, default=200,
+                   help="config 5 leg: timed steps of the on-GPU policy rollout (0 = skip)")
+    p.add_argument("--torch-policy-steps", type=int, default=50,
+                   help="config 5 comparison: timed steps with the PyTorch-ROCm policy (0 = skip)")
     return p.parse_args()
 
 
@@ -72,6 +76,93 @@ def cpu_baseline(window, seconds, procs):
             "sample": f"{procs} procs x {seconds:.0f} s: single-env BallEnv.step + prep_state4 (W={window}), "
                       f"13 static + 5 dynamic obstacles, uniform random 9-way actions, reset on done/1000 steps; "
                       f"{steps} env-steps in {el:.1f} s (oracle/py_ballenv.py, pure Python)"}
+
+
+def timed_graph_steps(graphs, steps, dev, stream, world):
+    """Replay graphs (steps in total), bracketed by barrier + synchronize; max over ranks."""
+    import torch
+    import torch.distributed as dist
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for g in graphs:
+        g.replay()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, ev0.elapsed_time(ev1) / steps
+
+
+def policy_leg(args, gb, dev, rank, world, stream):
+    """BASELINE config 5: the same env batch driven by the reference's Policy(W) on the GPU.
+
+    One step = be_policy_act (select_action, csrc/policy.hip) + be_step, both
+    writing into (T, N) trajectory rows, captured in HIP graphs.  The policy is
+    the reference's trained Policy(W) (tests/golden/policy_w{W}.npz) when the
+    fixture exists, else a random-init Policy(W).
+    """
+    import torch
+    from gym_ballenv_amd.policy import HipPolicy, Policy, reference_weights
+    N, W, T = args.envs, args.window, args.policy_steps
+    path = reference_weights(W)
+    torch.manual_seed(0)
+    pol = Policy.from_npz(path, W) if path else Policy(W)
+    res = {"workload": f"config 5: Policy({W}) select_action (be_policy_act, int8-MFMA fc1) + be_step, "
+                       f"{N} envs/GPU, T={T} steps per rollout, hipGraph replay",
+           "weights": os.path.relpath(path, ROOT) if path else "random init"}
+    env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
+    env.reset()
+    ro = gb.Rollout(env, pol, horizon=T, backend="hip", seed=0x5E1EC7)
+    ro.run_eager()                                   # warm-up rollout
+    ro.capture(chunk=min(T, 100))
+    ro.run()
+    el, ms = timed_graph_steps(ro._graphs, T, dev, stream, world)
+    res.update({"value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
+                "gpu_us_per_step": ms * 1e3})
+    # the policy kernel alone (same stream, graph of T launches)
+    hp = ro.hp
+    g = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(dev)
+    import ctypes as C
+    with torch.cuda.graph(g, stream=cap):
+        sp = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        for _ in range(T):
+            hp._lib.be_policy_act(hp._h, C.byref(env._st), env.obs.data_ptr(), C.byref(ro._act_outs[0]), 7, sp)
+    g.replay()
+    _, pms = timed_graph_steps([g], T, dev, stream, world)
+    H = pol.hidden_layer
+    flops = 2.0 * N * (4 + W * W) * H * 3           # int8 MFMA ops issued for fc1 (3 digit passes)
+    res.update({"policy_kernel_us": pms * 1e3, "packed_weight_bytes": hp.packed_bytes,
+                "fc1_int8_tops": flops / (pms * 1e-3) / 1e12})
+    episodes = env.episode_stats()
+    res["episodes"] = {k: episodes[k] for k in ("episodes", "mean_return", "mean_length")}
+    del g
+    ro.close()
+    env.close()
+    if args.torch_policy_steps > 0:
+        Tt = args.torch_policy_steps
+        env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
+        env.reset()
+        ro = gb.Rollout(env, pol, horizon=Tt, backend="torch")
+        ro.run_eager()
+        ro.capture(chunk=Tt)
+        ro.run()
+        el_t, _ = timed_graph_steps(ro._graphs, Tt, dev, stream, world)
+        res["torch_policy"] = {"value": Tt * N * world / el_t, "unit": "env-steps/s", "ms_per_step": el_t / Tt * 1e3,
+                               "what": "same loop with select_action in PyTorch-ROCm fp32 (Linear/softmax/cumsum "
+                                       "draw), hipGraph replay"}
+        ro.close()
+        env.close()
+    return res
 
 
 def main():
@@ -178,6 +269,8 @@ def main():
         if d.get("envs") == N and d.get("window") == W:
             traffic, traffic_src = d.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT)
 
+    pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
+
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), batch=65536 envs, window=10; achieved HBM GB/s",
@@ -197,6 +290,7 @@ def main():
                          "kernel": f"be_kernel<{W}, 0> (MODE_STEP)", "traffic_source": traffic_src},
             "cpu_baseline": base,
             "episodes": ep,
+            "policy_rollout": pol_res,
         }
         print(json.dumps(line), flush=True)
     env.close()

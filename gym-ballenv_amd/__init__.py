@@ -25,6 +25,12 @@ def __getattr__(name):
     if name in ("BallEnv", "make", "TimeLimit", "ENV_ID"):
         from . import envs
         return getattr(envs, name)
+    if name in ("Policy", "HipPolicy", "torch_select_action"):
+        from . import policy
+        return getattr(policy, name)
+    if name == "Rollout":
+        from .rollout import Rollout
+        return Rollout
     if name in ("shard", "gather_stats", "combine_stats"):
         from . import distributed
         return getattr(distributed, name)
@@ -32,4 +38,5 @@ def __getattr__(name):
 
 
 __all__ = ["EnvConfig", "MOVE_LIST", "step_bytes", "survey_step_bytes", "Box", "Discrete", "BallEnvError", "BatchedBallEnv",
-           "BallEnv", "make", "TimeLimit", "shard", "gather_stats", "combine_stats"]
+           "BallEnv", "make", "TimeLimit", "shard", "gather_stats", "combine_stats", "Policy", "HipPolicy",
+           "torch_select_action", "Rollout"]

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_STATIC, MAX_DYNAMIC, MAX_GOALS, MAX_ACTIONS, MAX_WINDOW = 64, 32, 16, 16, 64
 
 BE_OK, BE_E_INVALID, BE_E_HIP, BE_E_NOMEM, BE_E_DEVICE = 0, -1, -2, -3, -4
@@ -18,13 +18,15 @@ STATUS_BITS = {1: "reset tape exhausted", 2: "reset rejection limit", 4: "action
                16: "goal change with no other goal (the reference raises ValueError)"}
 
 LIB_NAME = "libballenv.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.realpath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("BALLENV_LIB") or os.path.join(os.path.dirname(os.path.realpath(__file__)), LIB_NAME)
+# BALLENV_LIB: load a diagnostics build (tools/) instead of the in-tree libballenv.so
 
 # Names declared in include/ballenv.h (checked by tests/test_abi.py).
 EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_bytes", "be_stats_slots",
            "be_last_error",
            "be_create", "be_destroy", "be_reset", "be_step", "be_observe", "be_sample_actions",
-           "be_status")
+           "be_status", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
+           "be_policy_bytes")
 
 
 class BeConfig(C.Structure):
@@ -56,6 +58,10 @@ class BeOut(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("obs_f32", C.c_void_p), ("reward", C.c_void_p), ("done", C.c_void_p),
                 ("truncated", C.c_void_p), ("terminal_obs", C.c_void_p), ("final_return", C.c_void_p),
                 ("final_len", C.c_void_p), ("stats", C.c_void_p)]
+
+
+class BeActOut(C.Structure):
+    _fields_ = [("action", C.c_void_p), ("log_prob", C.c_void_p), ("value", C.c_void_p), ("probs", C.c_void_p)]
 
 
 class BallEnvError(RuntimeError):
@@ -90,6 +96,11 @@ def lib() -> C.CDLL:
         "be_observe": (C.c_int, [vp, P(BeState), P(BeOut), vp]),
         "be_sample_actions": (C.c_int, [vp, vp, i32, u64, vp]),
         "be_status": (C.c_int, [vp, P(i32), vp]),
+        "be_policy_create": (C.c_int, [vp, i32, i32, P(vp)]),
+        "be_policy_destroy": (C.c_int, [vp]),
+        "be_policy_load": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "be_policy_act": (C.c_int, [vp, P(BeState), vp, P(BeActOut), u64, vp]),
+        "be_policy_bytes": (i64, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

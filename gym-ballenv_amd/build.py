@@ -11,6 +11,7 @@ import sys
 PKG = os.path.dirname(os.path.realpath(__file__))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "ballenv.hip")
+DEPS = [os.path.join(PKG, "csrc", "policy.hip")]
 HDR = os.path.join(ROOT, "include", "ballenv.h")
 OUT = os.path.join(PKG, "libballenv.so")
 ARCH = os.environ.get("BALLENV_OFFLOAD_ARCH", "gfx950")
@@ -27,7 +28,7 @@ def _stale(out, deps):
 
 
 def build_library(force: bool = False, verbose: bool = True) -> str:
-    if force or _stale(OUT, [SRC, HDR, __file__]):
+    if force or _stale(OUT, [SRC, HDR, __file__, *DEPS]):
         hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
         cmd = [hipcc, *HIPCC_FLAGS, "-I", os.path.join(ROOT, "include"), SRC, "-o", OUT + ".tmp"]
         if verbose:

@@ -1827,3 +1827,6 @@ int be_status(be_ctx* ctx, int32_t* status_out, void* stream) {
 }
 
 }  // extern "C"
+
+// on-GPU select_action (Policy forward + Categorical draw) for the batched rollout
+#include "policy.hip"

@@ -1,0 +1,141 @@
+"""On-GPU policy rollouts of a BatchedBallEnv (BASELINE config 5).
+
+The reference's A2C driver (examples/ball_cnn_ac3.py:573-600) runs one env on
+the host: per step ``prep_state4`` -> ``.to(device)`` -> ``select_action`` ->
+``.item()`` -> ``env.step``, and keeps ``policy.saved_actions`` /
+``policy.rewards`` lists for ``finish_episode`` (:222-246).  Here a step of all
+N envs is two launches that never leave the GPU:
+
+    be_policy_act   obs (N, 4+W*W) u8  ->  action, log_prob, value   (HipPolicy)
+    be_step         action             ->  obs, reward, done          (BatchedBallEnv)
+
+and each launch writes straight into row t of the (T, N) trajectory buffers
+(per-step ``be_out`` / ``be_act_out`` structs point into them: no copy
+kernels).  ``capture()`` records the T-step loop into HIP graphs, so
+``run()`` is one graph replay per chunk with no host work per step.
+
+``backend="torch"`` runs select_action as plain PyTorch fp32 (``Policy`` +
+``torch_select_action`` on ``torch.rand`` uniforms) -- the PyTorch-ROCm policy
+the BASELINE config names, kept as the comparison point.
+
+``discounted_returns`` is the batched form of finish_episode's return
+recursion (:224-227) with episode boundaries (done) cutting the sum.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _abi
+from .policy import HipPolicy, Policy, torch_select_action
+
+
+class Rollout:
+    def __init__(self, env, policy: Policy, horizon: int, backend: str = "hip", record_obs: bool = False,
+                 seed: int = 0x5E1EC7):
+        if backend not in ("hip", "torch"):
+            raise ValueError("backend must be 'hip' or 'torch'")
+        self.env, self.policy, self.T, self.backend = env, policy, int(horizon), backend
+        dev, N, T = env.device, env.num_envs, self.T
+        self.seed = int(seed)
+        self.actions = torch.zeros(T, N, dtype=torch.uint8, device=dev)
+        self.log_probs = torch.zeros(T, N, dtype=torch.float32, device=dev)
+        self.values = torch.zeros(T, N, dtype=torch.float32, device=dev)
+        self.rewards = torch.zeros(T, N, dtype=torch.float64, device=dev)
+        self.dones = torch.zeros(T, N, dtype=torch.bool, device=dev)
+        self.obs = torch.zeros(T + 1, N, env.obs_dim, dtype=torch.uint8, device=dev) if record_obs else None
+        self._graphs = []
+        self._lib = _abi.lib()
+        if backend == "hip":
+            self.hp = HipPolicy(env, policy, seed=self.seed)
+            self._act_outs = [_abi.BeActOut(self.actions[t].data_ptr(), self.log_probs[t].data_ptr(),
+                                            self.values[t].data_ptr(), None) for t in range(T)]
+        else:
+            self.hp = None
+            self.policy = policy.to(dev)     # draws: torch.rand on the default (graph-safe) generator
+        o = env._out
+        self._step_outs = []
+        for t in range(T):
+            obs_ptr = self.obs[t + 1].data_ptr() if record_obs else o.obs
+            self._step_outs.append(_abi.BeOut(obs_ptr, o.obs_f32, self.rewards[t].data_ptr(),
+                                              self.dones[t].data_ptr(), o.truncated, o.terminal_obs,
+                                              o.final_return, o.final_len, o.stats))
+
+    def _obs_t(self, t: int) -> torch.Tensor:
+        return self.obs[t] if self.obs is not None else self.env.obs
+
+    def step(self, t: int, stream_ptr=None) -> None:
+        """select_action + env step of every env, results into row t."""
+        env, lib = self.env, self._lib
+        s = env._stream() if stream_ptr is None else stream_ptr
+        obs = self._obs_t(t)
+        if self.backend == "hip":
+            rc = lib.be_policy_act(self.hp._h, C.byref(env._st), obs.data_ptr(), C.byref(self._act_outs[t]),
+                                   self.seed & (2**64 - 1), s)
+            if rc:
+                _abi.check(rc, env._ctx)
+        else:
+            with torch.no_grad():
+                u = torch.rand(env.num_envs, device=env.device)
+                a, lp, v, _ = torch_select_action(self.policy, obs, u)
+                self.actions[t].copy_(a)
+                self.log_probs[t].copy_(lp)
+                self.values[t].copy_(v)
+        rc = lib.be_step(env._ctx, C.byref(env._st), C.c_void_p(self.actions[t].data_ptr()), None, None,
+                         C.byref(self._step_outs[t]), s)
+        if rc:
+            _abi.check(rc, env._ctx)
+
+    def begin(self) -> None:
+        """Make row 0 of the obs record the env's current obs (call after reset)."""
+        if self.obs is not None:
+            self.obs[0].copy_(self.env.obs)
+
+    def run_eager(self) -> None:
+        self.begin()
+        for t in range(self.T):
+            self.step(t)
+
+    def capture(self, chunk: int = 250) -> None:
+        """Record the T steps into HIP graphs of ``chunk`` steps each."""
+        dev = self.env.device
+        if self.backend == "torch":
+            # initialise the BLAS handles eagerly: hipBLASLt set-up is not capturable
+            with torch.no_grad():
+                self.policy(self.env.obs[:64].float())
+            torch.cuda.synchronize(dev)
+        cap = torch.cuda.Stream(dev)
+        self._graphs = []
+        for c0 in range(0, self.T, chunk):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                sp = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+                for t in range(c0, min(self.T, c0 + chunk)):
+                    self.step(t, sp)
+            self._graphs.append(g)
+        torch.cuda.synchronize(dev)
+
+    def run(self) -> None:
+        """Replay the captured horizon (capture() first)."""
+        if not self._graphs:
+            raise RuntimeError("capture() first")
+        self.begin()
+        for g in self._graphs:
+            g.replay()
+
+    def discounted_returns(self, gamma: float = 0.99, bootstrap: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """R_t = r_t + gamma * R_{t+1} * (1 - done_t), per env (finish_episode, ball_cnn_ac3.py:224-227)."""
+        R = torch.zeros(self.env.num_envs, dtype=torch.float64, device=self.env.device) if bootstrap is None \
+            else bootstrap.to(torch.float64).clone()
+        out = torch.empty_like(self.rewards)
+        for t in range(self.T - 1, -1, -1):
+            R = self.rewards[t] + gamma * R * (~self.dones[t]).to(torch.float64)
+            out[t] = R
+        return out
+
+    def close(self) -> None:
+        self._graphs = []
+        if self.hp is not None:
+            self.hp.close()

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BE_ABI_VERSION 3
+#define BE_ABI_VERSION 4
 
 #define BE_MAX_STATIC   64
 #define BE_MAX_DYNAMIC  32
@@ -181,6 +181,39 @@ int be_sample_actions(be_ctx* ctx, uint8_t* actions_out, int32_t steps, uint64_t
 
 /* Synchronise the stream and read (then clear) the device status word. */
 int be_status(be_ctx* ctx, int32_t* status_out, void* stream);
+
+/* ---- on-GPU select_action for batched rollouts (BASELINE config 5) ----
+ * Replaces, for every env at once, the caller's per-step
+ *   probs, value = Policy(W)(prep_state4(state))      examples/ball_cnn_ac3.py:109-146
+ *   action ~ Categorical(probs); saved log_prob, value  ball_cnn_ac3.py:210-220
+ * (the reference runs it per single env with a host round trip per step,
+ * ball_cnn_ac3.py:573-600).  fc1 runs on the int8 matrix cores against a
+ * 24-bit fixed-point image of the fp32 weights (see csrc/policy.hip); the heads,
+ * softmax and log_prob are fp32.  The draw is an inverse-CDF of a Philox uniform
+ * keyed by (seed; global env id, episode, ep_len), so it is reproducible and
+ * independent of GPU count and graph replay.                                     */
+typedef struct be_policy be_policy;
+
+typedef struct be_act_out {
+  uint8_t* action;   /* (N) u8 sampled action index (feeds be_step's actions) */
+  float* log_prob;   /* (N) f32 log probs[action], or NULL */
+  float* value;      /* (N) f32 value_head output, or NULL */
+  float* probs;      /* (N, A) f32 softmax probabilities, or NULL */
+} be_act_out;
+
+/* A policy for ctx's window (inputs 4+W*W <= 128), hidden <= 256, actions <= 15. */
+int be_policy_create(be_ctx* ctx, int32_t hidden, int32_t num_actions, be_policy** out);
+int be_policy_destroy(be_policy* pol);
+/* (Re)load weights from DEVICE f32 arrays in torch state_dict layout:
+ * fc1_w (H, 4+W*W), fc1_b (H), act_w (A, H), act_b (A), val_w (1, H), val_b (1).
+ * Asynchronous on stream (one packing kernel); graph-capturable.                  */
+int be_policy_load(be_policy* pol, const float* fc1_w, const float* fc1_b, const float* act_w, const float* act_b,
+                   const float* val_w, const float* val_b, void* stream);
+/* Policy forward + draw for every env from obs (N, 4+W*W) u8; st supplies episode/ep_len (Philox key). */
+int be_policy_act(be_policy* pol, const be_state* st, const uint8_t* obs, const be_act_out* out, uint64_t seed,
+                  void* stream);
+/* Bytes of the packed weight image (staged once per workgroup in LDS). */
+int64_t be_policy_bytes(const be_policy* pol);
 
 #ifdef __cplusplus
 }

@@ -51,7 +51,7 @@
  *                   sub = 1<<22 | k<<12 | a: static k attempt a (x, y) | sub = 2<<22 | k<<12: dynamic k
  *   reset (tape)    the reference's single sequential stream
  *   be_sample_actions: c1 = t, c2 = 0                                              */
-enum { PURPOSE_STEP_OBS = 1, PURPOSE_ACTION = 2, PURPOSE_RESET = 3, PURPOSE_SAMPLE = 4 };
+enum { PURPOSE_STEP_OBS = 1, PURPOSE_ACTION = 2, PURPOSE_RESET = 3, PURPOSE_SAMPLE = 4, PURPOSE_POLICY = 5 };
 
 static void philox4x32_10(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
   uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
@@ -426,4 +426,16 @@ int orc_sample_actions(const be_config* c, uint8_t* out, int32_t steps, uint64_t
 /* exposed for the exhaustive Philox/known-answer tests */
 void orc_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
   philox4x32_10(ctr, k0, k1, out);
+}
+
+/* The uniform behind be_policy_act's Categorical draw for env i (select_action,
+ * examples/ball_cnn_ac3.py:210-220): word 0 of Philox(seed; gid, episode, ep_len,
+ * POLICY<<24), top 24 bits / 2^24, in [0, 1).  The draw itself (inverse CDF of
+ * the fp32 probs) is restated in torch by gym_ballenv_amd.policy.torch_select_action. */
+int orc_policy_uniforms(const be_config* c, const uint32_t* episode, const int32_t* ep_len, uint64_t seed,
+                        float* u_out) {
+  for (int32_t i = 0; i < c->num_envs; ++i)
+    u_out[i] = (float)(philox_word(seed, (uint32_t)(c->env_offset + i), episode[i], (uint32_t)ep_len[i],
+                                   PURPOSE_POLICY, 0, 0) >> 8) * (1.0f / 16777216.0f);
+  return 0;
 }

@@ -41,6 +41,7 @@ def lib():
         L.orc_observe.argtypes = [vp, vp, vp]
         L.orc_sample_actions.argtypes = [vp, vp, i32, u64]
         L.orc_philox4x32_10.argtypes = [vp, C.c_uint32, C.c_uint32, vp]
+        L.orc_policy_uniforms.argtypes = [vp, vp, vp, u64, vp]
         _lib = L
     return _lib
 
@@ -112,3 +113,12 @@ def philox(ctr, key):
     o = np.zeros(4, np.uint32)
     lib().orc_philox4x32_10(_p(c), int(key[0]), int(key[1]), _p(o))
     return [int(v) for v in o]
+
+
+def policy_uniforms(cfg, episode, ep_len, seed):
+    """(N,) f32 uniforms of be_policy_act's draws for the given per-env key words."""
+    ep = np.ascontiguousarray(episode, dtype=np.uint32)
+    ln = np.ascontiguousarray(ep_len, dtype=np.int32)
+    u = np.zeros(cfg.num_envs, np.float32)
+    lib().orc_policy_uniforms(C.byref(cfg), _p(ep), _p(ln), int(seed), _p(u))
+    return u
