@@ -1,23 +1,30 @@
 """In-tree build of libballenv.so (gfx950) -- also run by __graft_entry__.build().
 
     python -m gym_ballenv_amd.build [--force]
+
+Two translation units, compiled separately (each embeds its own gfx950 code
+object) and linked into one shared library:
+  csrc/ballenv.hip  step / reset / observe kernels + the C ABI
+  csrc/policy.hip   select_action kernel (-fno-slp-vectorize: scalar f32 FMAs
+                    interleave better with MFMAs than SLP-packed ones on gfx950)
 """
 from __future__ import annotations
 
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.realpath(__file__))
 ROOT = os.path.dirname(PKG)
-SRC = os.path.join(PKG, "csrc", "ballenv.hip")
-DEPS = [os.path.join(PKG, "csrc", "policy.hip")]
+CSRC = os.path.join(PKG, "csrc")
 HDR = os.path.join(ROOT, "include", "ballenv.h")
 OUT = os.path.join(PKG, "libballenv.so")
 ARCH = os.environ.get("BALLENV_OFFLOAD_ARCH", "gfx950")
 
-HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
-               f"--offload-arch={ARCH}"]
+BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}"]
+UNITS = {"ballenv.hip": [], "policy.hip": ["-fno-slp-vectorize"]}
+HEADERS = [HDR, os.path.join(CSRC, "philox.h"), os.path.join(CSRC, "internal.h")]
 
 
 def _stale(out, deps):
@@ -27,15 +34,31 @@ def _stale(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_library(force: bool = False, verbose: bool = True) -> str:
-    if force or _stale(OUT, [SRC, HDR, __file__, *DEPS]):
-        hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-        cmd = [hipcc, *HIPCC_FLAGS, "-I", os.path.join(ROOT, "include"), SRC, "-o", OUT + ".tmp"]
+def build_library(force: bool = False, verbose: bool = True, extra_flags=(), out: str = OUT) -> str:
+    srcs = [os.path.join(CSRC, u) for u in UNITS]
+    if not (force or extra_flags or _stale(out, [*srcs, *HEADERS, __file__])):
+        return out
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    objs, cmds = [], []
+    for u, flags in UNITS.items():
+        obj = f"{out}.{os.path.splitext(u)[0]}.o"
+        objs.append(obj)
+        cmds.append([hipcc, *BASE_FLAGS, *flags, *extra_flags, *inc, "-c", os.path.join(CSRC, u), "-o", obj])
+
+    def run(cmd):
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-        os.replace(OUT + ".tmp", OUT)
-    return OUT
+
+    with ThreadPoolExecutor(len(cmds)) as ex:
+        list(ex.map(run, cmds))
+    link = [hipcc, "-shared", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp"]
+    run(link)
+    os.replace(out + ".tmp", out)
+    for o in objs:
+        os.remove(o)
+    return out
 
 
 if __name__ == "__main__":

@@ -48,6 +48,8 @@
 #include <string.h>
 
 #include "ballenv.h"
+#include "internal.h"
+#include "philox.h"
 
 namespace {
 
@@ -156,26 +158,8 @@ __device__ __forceinline__ int isqrt_small(int n) {  // floor(sqrt(n)), 0 <= n <
 }
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
-struct u4 { uint32_t x, y, z, w; };
 typedef short v2s __attribute__((ext_vector_type(2)));   // a packed (x, y) int16 position
 
-// Philox4x32-10 (Salmon et al., SC'11); same as oracle/ballenv_oracle.c
-__device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, unsigned long long seed) {
-  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  // keep the key schedule in VGPRs: hoisted into SGPRs it pins 20 scalar registers and spills
-  asm volatile("" : "+v"(k0), "+v"(k1));
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    // one v_mad_u64_u32 per product instead of a mul_hi + mul_lo pair
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-  }
-  return u4{c0, c1, c2, c3};
-}
-__device__ __forceinline__ uint32_t tag(uint32_t purpose, uint32_t sub) { return (purpose << 24) | (sub & 0xFFFFFFu); }
 __device__ __forceinline__ uint32_t pick_word(const u4& b, int w) {
   return w == 0 ? b.x : (w == 1 ? b.y : (w == 2 ? b.z : b.w));
 }
@@ -1531,6 +1515,15 @@ static int fail(be_ctx* ctx, int code, const char* fmt, const char* detail) {
     if (e_ != hipSuccess) return fail(ctx, BE_E_HIP, "HIP error: %s", hipGetErrorString(e_)); \
   } while (0)
 
+// library-internal accessors for the other translation units (csrc/internal.h)
+be_ctx_view be_ctx_get(const be_ctx* ctx) {
+  be_ctx_view v;
+  v.num_envs = ctx->cfg.num_envs; v.window = ctx->cfg.window; v.device = ctx->device;
+  v.env_offset = ctx->cfg.env_offset;
+  return v;
+}
+int be_ctx_fail(be_ctx* ctx, int code, const char* msg) { return fail(ctx, code, "%s", msg); }
+
 extern "C" {
 
 int be_abi_version(void) { return BE_ABI_VERSION; }
@@ -1827,6 +1820,3 @@ int be_status(be_ctx* ctx, int32_t* status_out, void* stream) {
 }
 
 }  // extern "C"
-
-// on-GPU select_action (Policy forward + Categorical draw) for the batched rollout
-#include "policy.hip"

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Diagnostics builds of libballenv.so with other policy tile counts (BE_POL_TILES) -> tools/diag/
+# Diagnostics builds of libballenv.so with extra compile flags -> tools/diag/libballenv_<NAME>.so
+# each argument: NAME:FLAGS, e.g. u1:-DBE_POL_UNROLL=1
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/diag
-# each argument: NAME:FLAGS, e.g. T2:-DBE_POL_TILES=2  T2u:"-DBE_POL_TILES=2 -DBE_POL_UNROLL=13"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math --offload-arch=gfx950 \
-      $flags -I include gym-ballenv_amd/csrc/ballenv.hip -o tools/diag/libballenv_$name.so &
+  python3 -c "import sys; sys.path.insert(0, '.'); from gym_ballenv_amd.build import build_library; \
+build_library(verbose=False, extra_flags='$flags'.split(), out='tools/diag/libballenv_$name.so')" &
 done
 wait
