@@ -19,7 +19,10 @@ kernels).  ``capture()`` records the T-step loop into HIP graphs, so
 the BASELINE config names, kept as the comparison point.
 
 ``discounted_returns`` is the batched form of finish_episode's return
-recursion (:224-227) with episode boundaries (done) cutting the sum.
+recursion (:224-227) with episode boundaries (done) cutting the sum;
+``a2c_losses`` / ``a2c_update`` are the whole finish_episode (per-episode
+return normalisation, policy + value losses) over all envs at once, so a
+training loop is rollout (HIP) -> update (torch autograd) -> re-pack (HIP).
 """
 from __future__ import annotations
 
@@ -139,3 +142,65 @@ class Rollout:
         self._graphs = []
         if self.hp is not None:
             self.hp.close()
+
+
+def a2c_losses(policy: Policy, obs: torch.Tensor, actions: torch.Tensor, rewards: torch.Tensor,
+               dones: torch.Tensor, gamma: float = 0.99, eps: Optional[float] = None):
+    """Batched ``finish_episode`` (examples/ball_cnn_ac3.py:222-246) over a recorded rollout.
+
+    obs (T, N, F) u8 -- the obs each action was chosen from; actions (T, N); rewards (T, N)
+    f64; dones (T, N) bool.  Every maximal run of an env's steps that ends at a done (or at
+    the horizon) is one episode, as ``policy.rewards`` / ``policy.saved_actions`` are in the
+    reference.  Per episode, exactly as there:
+      R_t = r_t + gamma R_{t+1} (python floats), then torch.tensor(R) (fp32),
+      R^ = (R - R.mean()) / (R.std() + eps)          (unbiased std, eps = fp32 eps),
+      policy loss  sum_t -log pi(a_t|s_t) * (R^_t - v_t.item()),
+      value loss   sum_t smooth_l1(v_t, R^_t).
+    Episodes of one step are skipped (the driver only trains when t > 0, :614).
+    log pi and v are recomputed from ``obs`` with autograd (the rollout's own values are
+    the same forward, taken without a graph).  Returns (policy_loss, value_loss) sums.
+    """
+    import numpy as np
+    eps = float(np.finfo(np.float32).eps) if eps is None else eps
+    T, N = rewards.shape
+    dev = rewards.device
+    d64 = dones.to(torch.float64)
+    R = torch.empty(T, N, dtype=torch.float64, device=dev)
+    acc = torch.zeros(N, dtype=torch.float64, device=dev)
+    for t in range(T - 1, -1, -1):
+        acc = rewards[t].to(torch.float64) + gamma * acc * (1.0 - d64[t])
+        R[t] = acc
+    R32 = R.to(torch.float32)
+    # episode id of every (t, env): dones strictly before t in that env, then env
+    seg = (torch.cumsum(dones.to(torch.int64), 0) - dones.to(torch.int64)) * N + torch.arange(N, device=dev)
+    _, sid = torch.unique(seg.reshape(-1), return_inverse=True)
+    S = int(sid.max()) + 1
+    flat = R32.reshape(-1)
+    cnt = torch.bincount(sid, minlength=S).to(torch.float32)
+    mean = torch.zeros(S, device=dev).index_add_(0, sid, flat) / cnt
+    dev2 = (flat - mean[sid]) ** 2
+    var = torch.zeros(S, device=dev).index_add_(0, sid, dev2) / (cnt - 1).clamp(min=1)
+    valid = (cnt > 1)[sid]
+    Rn = (flat - mean[sid]) / (var.sqrt()[sid] + eps)
+    probs, v = policy(obs.reshape(T * N, -1).float())
+    v = v.squeeze(-1)
+    logp = torch.log(probs.gather(-1, actions.reshape(-1, 1).long()).squeeze(-1))
+    adv = Rn - v.detach()
+    pl = -(logp * adv)[valid].sum()
+    vl = torch.nn.functional.smooth_l1_loss(v[valid], Rn[valid], reduction="sum")
+    return pl, vl
+
+
+def a2c_update(rollout: "Rollout", optimizer, gamma: float = 0.99):
+    """One A2C step on a recorded rollout (record_obs=True): loss.backward(), optimizer.step(),
+    then re-pack the new weights for the HIP policy kernel.  Returns the loss value."""
+    if rollout.obs is None:
+        raise ValueError("a2c_update needs Rollout(record_obs=True)")
+    pl, vl = a2c_losses(rollout.policy, rollout.obs[:-1], rollout.actions, rollout.rewards, rollout.dones, gamma)
+    loss = pl + vl
+    optimizer.zero_grad()
+    loss.backward()
+    optimizer.step()
+    if rollout.hp is not None:
+        rollout.hp.load(rollout.policy)
+    return float(loss.detach())

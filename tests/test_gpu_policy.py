@@ -180,3 +180,25 @@ def test_rollout_torch_backend_runs(gpu):
     assert int(ro.actions.max()) < 9
     env.status()
     ro.close(); env.close()
+
+
+def test_a2c_update_on_gpu_rollout(gpu):
+    """rollout (HIP) -> a2c_update (torch autograd on the recorded obs) -> re-pack: the loss is
+    finite, the weights move, and the HIP kernel then acts with the new weights."""
+    import copy
+    from gym_ballenv_amd import Rollout, a2c_update
+    from gym_ballenv_amd.policy import Policy, reference_weights
+    pol = Policy.from_npz(reference_weights(10), 10).to(gpu)
+    w0 = copy.deepcopy(pol.state_dict())
+    env = make(gpu, 512, 10, seed=3)
+    ro = Rollout(env, pol, horizon=32, backend="hip", record_obs=True, seed=2)
+    ro.run_eager()
+    opt = torch.optim.Adam(pol.parameters(), lr=1e-2)
+    loss = a2c_update(ro, opt, gamma=0.99)
+    assert np.isfinite(loss)
+    assert not torch.equal(w0["fc1.weight"], pol.fc1.weight.detach())
+    from gym_ballenv_amd.policy import HipPolicy
+    hp2 = HipPolicy(env, pol, probs=True)
+    a_new = check_act(env, pol.cpu(), hp2, env.obs, seed=9)
+    assert torch.equal(ro.hp.act(seed=9)[0].cpu(), a_new)      # the rollout's kernel was re-packed
+    hp2.close(); ro.close(); env.close()
