@@ -26,7 +26,7 @@ EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_by
            "be_last_error",
            "be_create", "be_destroy", "be_reset", "be_step", "be_observe", "be_sample_actions",
            "be_status", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
-           "be_policy_bytes")
+           "be_policy_bytes", "be_observe_blocks")
 
 
 class BeConfig(C.Structure):
@@ -101,6 +101,7 @@ def lib() -> C.CDLL:
         "be_policy_load": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
         "be_policy_act": (C.c_int, [vp, P(BeState), vp, P(BeActOut), u64, vp]),
         "be_policy_bytes": (i64, [vp]),
+        "be_observe_blocks": (C.c_int, [vp, P(BeState), vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -184,6 +184,21 @@ class BatchedBallEnv:
         _abi.check(self._lib.be_observe(self._ctx, C.byref(self._st), C.byref(self._out), self._stream()), self._ctx)
         return self.obs_f32 if self._want_f32 else self.obs
 
+    def observe_blocks(self, f32: bool = False) -> torch.Tensor:
+        """prep_state2 of examples/ball_env_reinforce.py:130-172 for the current state:
+        (N, 29) block counts (u8, or f32 with ``f32=True``) -- the input of the
+        REINFORCE / supervised policies (29 = 4 quadrant + 5x5 blocks)."""
+        dt = torch.float32 if f32 else torch.uint8
+        out = torch.empty(self.num_envs, 29, dtype=dt, device=self.device)
+        u8, f = (None, out.data_ptr()) if f32 else (out.data_ptr(), None)
+        _abi.check(self._lib.be_observe_blocks(self._ctx, C.byref(self._st), u8, f, self._stream()), self._ctx)
+        return out
+
+    def window_only(self) -> torch.Tensor:
+        """(N, W*W) view of the window part of the obs: prep_state4 as the potential-field
+        planners define it, without the quadrant (examples/potential_fields_modified.py:66-93)."""
+        return (self.obs_f32 if self._want_f32 else self.obs)[:, 4:]
+
     def sample_actions(self, steps: int, seed: int = 0xBA11) -> torch.Tensor:
         """(steps, N) u8 uniform action indices from Philox(seed; global env id, t)."""
         out = torch.empty(steps, self.num_envs, dtype=torch.uint8, device=self.device)

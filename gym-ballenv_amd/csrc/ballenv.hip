@@ -1519,10 +1519,13 @@ static int fail(be_ctx* ctx, int code, const char* fmt, const char* detail) {
 be_ctx_view be_ctx_get(const be_ctx* ctx) {
   be_ctx_view v;
   v.num_envs = ctx->cfg.num_envs; v.window = ctx->cfg.window; v.device = ctx->device;
+  v.num_static = ctx->cfg.num_static; v.num_dynamic = ctx->cfg.num_dynamic;
   v.env_offset = ctx->cfg.env_offset;
   return v;
 }
 int be_ctx_fail(be_ctx* ctx, int code, const char* msg) { return fail(ctx, code, "%s", msg); }
+static int check_state(be_ctx* ctx, const be_state* st);
+int be_ctx_check_state(be_ctx* ctx, const be_state* st) { return check_state(ctx, st); }
 
 extern "C" {
 

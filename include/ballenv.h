@@ -215,6 +215,12 @@ int be_policy_act(be_policy* pol, const be_state* st, const uint8_t* obs, const 
 /* Bytes of the packed weight image (staged once per workgroup in LDS). */
 int64_t be_policy_bytes(const be_policy* pol);
 
+/* ---- sibling observation formats (the reference's other callers) ----
+ * prep_state2 of examples/ball_env_reinforce.py:130-172 for every env's current state:
+ * (N, 29) block counts -- quadrant one-hot, [16] = 1 (the agent's cell), +1 per obstacle
+ * in its 20-px block of the 5x5 grid -- as u8 (out) and/or f32 (out_f32; NULL = skip). */
+int be_observe_blocks(be_ctx* ctx, const be_state* st, uint8_t* out, float* out_f32, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

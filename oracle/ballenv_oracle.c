@@ -439,3 +439,40 @@ int orc_policy_uniforms(const be_config* c, const uint32_t* episode, const int32
                                    PURPOSE_POLICY, 0, 0) >> 8) * (1.0f / 16777216.0f);
   return 0;
 }
+
+/* prep_state2 of examples/ball_env_reinforce.py:130-172 (with block_to_arrpos :169-172):
+ * the 29-input block-count encoding.  out[0:4] = quadrant one-hot (as prep_state4's),
+ * out[16] = 1 (the agent's own cell), then per obstacle (statics, then dynamics, i.e.
+ * state[3:]) with x_dist = ax - ox, y_dist = ay - oy: if both are non-zero,
+ * x_block = sign(x_dist) * (x_dist - 10) // 20 (floor division; likewise y), else both
+ * blocks are 0; if |x_block| < 3 and |y_block| < 3: out[4 + 12 + 5*y_block + x_block] += 1. */
+static int32_t floordiv20(int32_t a) { return a >= 0 ? a / 20 : -((-a + 19) / 20); }
+
+int orc_observe_blocks(const be_config* c, const be_state* st, uint8_t* out) {
+  const int32_t N = c->num_envs;
+  for (int32_t i = 0; i < N; ++i) {
+    uint8_t* row = out + (int64_t)i * 29;
+    memset(row, 0, 29);
+    const int32_t ax = pk_x(st->agent[i]), ay = pk_y(st->agent[i]);
+    const int32_t gx = pk_x(st->goal[i]), gy = pk_y(st->goal[i]);
+    const int32_t dx = gx - ax, dy = gy - ay;                          /* :139-150 */
+    if (dx >= 0 && dy >= 0) row[1] = 1;
+    else if (dx < 0 && dy >= 0) row[0] = 1;
+    else if (dx < 0 && dy < 0) row[3] = 1;
+    else row[2] = 1;
+    row[16] = 1;                                                       /* :138 */
+    const int32_t nobs = c->num_static + c->num_dynamic;
+    for (int32_t k = 0; k < nobs; ++k) {                               /* :152-165 */
+      const int32_t p = k < c->num_static ? st->static_obs[(int64_t)k * N + i]
+                                          : st->dyn_obs[(int64_t)(k - c->num_static) * N + i];
+      const int32_t xd = ax - pk_x(p), yd = ay - pk_y(p);
+      int32_t xb = 0, yb = 0;
+      if (xd != 0 && yd != 0) {
+        xb = floordiv20(xd > 0 ? xd - 10 : 10 - xd);
+        yb = floordiv20(yd > 0 ? yd - 10 : 10 - yd);
+      }
+      if (abs(xb) < 3 && abs(yb) < 3) row[4 + 12 + 5 * yb + xb] += 1;
+    }
+  }
+  return 0;
+}

@@ -42,6 +42,7 @@ def lib():
         L.orc_sample_actions.argtypes = [vp, vp, i32, u64]
         L.orc_philox4x32_10.argtypes = [vp, C.c_uint32, C.c_uint32, vp]
         L.orc_policy_uniforms.argtypes = [vp, vp, vp, u64, vp]
+        L.orc_observe_blocks.argtypes = [vp, vp, vp]
         _lib = L
     return _lib
 
@@ -122,3 +123,10 @@ def policy_uniforms(cfg, episode, ep_len, seed):
     u = np.zeros(cfg.num_envs, np.float32)
     lib().orc_policy_uniforms(C.byref(cfg), _p(ep), _p(ln), int(seed), _p(u))
     return u
+
+
+def observe_blocks(cfg, st):
+    """(N, 29) u8 prep_state2 block counts (examples/ball_env_reinforce.py:130-172)."""
+    out = np.zeros((cfg.num_envs, 29), np.uint8)
+    lib().orc_observe_blocks(C.byref(cfg), C.byref(_state_struct(st)), _p(out))
+    return out
