@@ -31,6 +31,9 @@ def __getattr__(name):
     if name in ("Rollout", "a2c_losses", "a2c_update"):
         from . import rollout
         return getattr(rollout, name)
+    if name == "BatchedBoard":
+        from .board import BatchedBoard
+        return BatchedBoard
     if name in ("shard", "gather_stats", "combine_stats"):
         from . import distributed
         return getattr(distributed, name)
@@ -39,4 +42,4 @@ def __getattr__(name):
 
 __all__ = ["EnvConfig", "MOVE_LIST", "step_bytes", "survey_step_bytes", "Box", "Discrete", "BallEnvError", "BatchedBallEnv",
            "BallEnv", "make", "TimeLimit", "shard", "gather_stats", "combine_stats", "Policy", "HipPolicy",
-           "torch_select_action", "Rollout", "a2c_losses", "a2c_update"]
+           "torch_select_action", "Rollout", "a2c_losses", "a2c_update", "BatchedBoard"]

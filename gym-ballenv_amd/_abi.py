@@ -26,7 +26,10 @@ EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_by
            "be_last_error",
            "be_create", "be_destroy", "be_reset", "be_step", "be_observe", "be_sample_actions",
            "be_status", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
-           "be_policy_bytes", "be_observe_blocks")
+           "be_policy_bytes", "be_observe_blocks",
+           "be_board_config_default", "be_board_create", "be_board_destroy", "be_board_last_error",
+           "be_board_reset", "be_board_step", "be_board_observe", "be_board_status")
+BOARD_MAX_STATIC, BOARD_MAX_ACTIONS, BOARD_FEATURES = 32, 16, 20
 
 
 class BeConfig(C.Structure):
@@ -62,6 +65,31 @@ class BeOut(C.Structure):
 
 class BeActOut(C.Structure):
     _fields_ = [("action", C.c_void_p), ("log_prob", C.c_void_p), ("value", C.c_void_p), ("probs", C.c_void_p)]
+
+
+class BeBoardConfig(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32), ("num_static", C.c_int32), ("env_offset", C.c_int64), ("seed", C.c_uint64),
+        ("screen_width", C.c_int32), ("screen_height", C.c_int32),
+        ("strip_obs_x", C.c_int32), ("strip_obs_y", C.c_int32),
+        ("strip_goal_x", C.c_int32), ("strip_goal_y", C.c_int32),
+        ("strip_agent_x", C.c_int32), ("strip_agent_y", C.c_int32),
+        ("agent_radius", C.c_double), ("static_radius", C.c_double), ("obstacle_feature_radius", C.c_double),
+        ("goal_threshold", C.c_double), ("min_spawn_dist", C.c_double),
+        ("spawn_thresh_agent", C.c_double), ("spawn_thresh_goal", C.c_double),
+        ("num_actions", C.c_int32), ("actions", (C.c_double * 2) * 16),
+        ("time_limit", C.c_int32), ("autoreset", C.c_int32),
+    ]
+
+
+class BeBoardState(C.Structure):
+    _fields_ = [("agent", C.c_void_p), ("goal", C.c_void_p), ("dist", C.c_void_p), ("total_dist", C.c_void_p),
+                ("ep_return", C.c_void_p), ("ep_len", C.c_void_p), ("episode", C.c_void_p),
+                ("static_obs", C.c_void_p)]
+
+
+class BeBoardOut(C.Structure):
+    _fields_ = [("features", C.c_void_p), ("reward", C.c_void_p), ("done", C.c_void_p), ("truncated", C.c_void_p)]
 
 
 class BallEnvError(RuntimeError):
@@ -102,6 +130,14 @@ def lib() -> C.CDLL:
         "be_policy_act": (C.c_int, [vp, P(BeState), vp, P(BeActOut), u64, vp]),
         "be_policy_bytes": (i64, [vp]),
         "be_observe_blocks": (C.c_int, [vp, P(BeState), vp, vp, vp]),
+        "be_board_config_default": (C.c_int, [P(BeBoardConfig), i32, i32]),
+        "be_board_create": (C.c_int, [P(BeBoardConfig), i32, P(vp)]),
+        "be_board_destroy": (C.c_int, [vp]),
+        "be_board_last_error": (C.c_char_p, [vp]),
+        "be_board_reset": (C.c_int, [vp, P(BeBoardState), vp, vp, i32, P(BeBoardOut), vp]),
+        "be_board_step": (C.c_int, [vp, P(BeBoardState), vp, vp, P(BeBoardOut), vp]),
+        "be_board_observe": (C.c_int, [vp, P(BeBoardState), P(BeBoardOut), vp]),
+        "be_board_status": (C.c_int, [vp, P(i32), vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -138,3 +174,9 @@ def step_bytes(c: BeConfig) -> int:
 
 def stats_slots(c: BeConfig) -> int:
     return int(lib().be_stats_slots(C.byref(c)))
+
+
+def board_check(rc: int, board=None) -> None:
+    if rc != BE_OK:
+        msg = lib().be_board_last_error(board)
+        raise BallEnvError(f"libballenv board error {rc}: {msg.decode() if msg else ''}")

@@ -8,6 +8,7 @@ object) and linked into one shared library:
   csrc/policy.hip   select_action kernel (-fno-slp-vectorize: scalar f32 FMAs
                     interleave better with MFMAs than SLP-packed ones on gfx950)
   csrc/features.hip sibling observation formats (prep_state2 block counts)
+  csrc/board.hip    the createBoard physics profile + featureExtractor
 """
 from __future__ import annotations
 
@@ -24,7 +25,7 @@ OUT = os.path.join(PKG, "libballenv.so")
 ARCH = os.environ.get("BALLENV_OFFLOAD_ARCH", "gfx950")
 
 BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}"]
-UNITS = {"ballenv.hip": [], "policy.hip": ["-fno-slp-vectorize"], "features.hip": []}
+UNITS = {"ballenv.hip": [], "policy.hip": ["-fno-slp-vectorize"], "features.hip": [], "board.hip": []}
 HEADERS = [HDR, os.path.join(CSRC, "philox.h"), os.path.join(CSRC, "internal.h")]
 
 

@@ -1,0 +1,386 @@
+// board.hip -- the createBoard physics profile, batched: N
+// independent ``ballenv_pygame.createBoard`` worlds stepped by one launch, each step
+// followed by ``featureExtractor.featureExtractor`` (the 20 IRL features step() computes).
+//
+// Reference (ballenv_pygame.py / featureExtractor.py):
+//   Obstacle.__init__            :21-50   x = randint(0, W), y = randint(0, H), rad 20, vel 0
+//   createBoard.reset            :460-513 goal / agent = generate_randomval (ranf), agent
+//                                          re-sampled while dist < 50 (state[2] keeps the first
+//                                          distance), statics rejected while within 15+20 of the
+//                                          agent or 5+20 of the goal (check_overlap :381-387)
+//   createBoard.step             :650-675 old = |agent-goal|; agent += action, clamp [0, W];
+//                                          state[2] = |agent-goal|; calc_reward; features
+//   createBoard.calc_reward      :680-706 any obstacle within 20 (<=) -> -1, done; else
+//                                          |agent-goal| < 15 -> +1, done; else (old-cur)/total
+//   featureExtractor             featureExtractor.py:247-265 (+ :36-193): [distance bin,
+//                                          relative goal direction x4, density x3, speed x
+//                                          orientation 3x3, social forces x3]
+//
+// Every coordinate is f64 as in the reference (ranf spawns; the actions are the integer
+// actionArray moves or arbitrary float deltas).  Distances are sqrt(fl(x*x) + fl(y*y)) --
+// math.sqrt(math.pow(x, 2) + math.pow(y, 2)) with correctly rounded pow(x, 2) and sqrt, no
+// FMA contraction -- so positions, rewards, returns and done are bit-exact.  The features
+// use hypot / acos / exp (1-ulp libraries on both sides): their bins and counts are exact
+// away from measure-zero boundaries and the social-force sum agrees to ~1e-16 relative.
+//
+// createBoard's velocities are identically zero (the agent's agent_x_vel is never changed,
+// :338; Obstacle vel defaults to 0, :40-47), so for every obstacle relvel = 0 -> speed bin 0
+// and angle_between(v1, 0) = arccos(0) = pi/2 -> orientation bin 1, and the social-force
+// factor lam + 0.5 (1 - lam)(1 + cos(pi/2)) is exactly 1.5 in f64 (featureExtractor.py:61-86,
+// 115-130, 170-193).  The kernel computes those terms from that identity.
+//
+// One lane per env; the env index is the unit-stride HBM axis of every array.  Resets
+// (reset(), or autoreset inside step) run on the env's own lane: sequential draws from a
+// tape (parity mode: the reference's ranf/randint values in call order) or Philox(seed;
+// gid, episode, 0, BOARD<<24 | block).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <new>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "ballenv.h"
+#include "philox.h"
+
+namespace {
+
+constexpr uint32_t PURPOSE_BOARD_RESET = 6;
+constexpr int BOARD_REJECT_LIMIT = 4096;
+constexpr double PI = 3.141592653589793;   // math.pi
+
+struct BoardTables {
+  double actions[BE_BOARD_MAX_ACTIONS][2];
+};
+
+struct BParams {
+  double* agent; double* goal; double* dist; double* total; double* ep_return;
+  int32_t* ep_len; uint32_t* episode; int32_t* statics;
+  float* features; double* reward; uint8_t* done; uint8_t* truncated;
+  const uint8_t* actions; const double* deltas; const uint8_t* mask;
+  const double* tape; int32_t tape_len;
+  const BoardTables* tables;
+  int* status;
+  unsigned long long seed;
+  int32_t n, ns, num_actions, time_limit, autoreset, gid0, mode;   // mode: 0 step, 1 reset, 2 observe
+  int32_t W, H, sox, soy, sgx, sgy, sax, say;
+  double r_collide, r_feature_obs, r_agent, goal_thr, min_spawn, thr_agent, thr_goal;
+};
+
+__device__ __forceinline__ double dist2(double x1, double y1, double x2, double y2) {
+  const double dx = x1 - x2, dy = y1 - y2;
+  return sqrt(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)));   // math.sqrt(math.pow(dx,2)+math.pow(dy,2))
+}
+__device__ __forceinline__ int sx(int32_t p) { return (int)(int16_t)(p & 0xFFFF); }
+__device__ __forceinline__ int sy(int32_t p) { return p >> 16; }
+
+// Sequential draw source of one reset: tape column (f64 values in call order) or Philox words.
+struct Draws {
+  const double* tape; int32_t len, n, env, cur;
+  uint32_t gid, episode; unsigned long long seed;
+  u4 blk; int32_t have;
+  int* status;
+  __device__ uint32_t word() {
+    if ((cur & 3) == 0) blk = philox(gid, episode, 0u, tag(PURPOSE_BOARD_RESET, (uint32_t)(cur >> 2)), seed);
+    const uint32_t w = (cur & 3) == 0 ? blk.x : ((cur & 3) == 1 ? blk.y : ((cur & 3) == 2 ? blk.z : blk.w));
+    ++cur;
+    return w;
+  }
+  __device__ double tape_next() {
+    if (cur >= len) { atomicOr(status, BE_STATUS_RESET_TAPE_EXHAUSTED); return 0.0; }
+    return tape[(int64_t)(cur++) * n + env];
+  }
+  __device__ double ranf() {   // np.random.ranf: 53-bit uniform in [0, 1)
+    if (tape) return tape_next();
+    const uint32_t a = word() >> 5, b = word() >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+  }
+  __device__ int randint(int lo, int hi) {
+    if (tape) return (int)tape_next();
+    return lo + (int)__umulhi(word(), (uint32_t)(hi - lo));
+  }
+};
+
+// featureExtractor(state, obstacle_list, (0, 0), agent_rad) -> 20 f32 (featureExtractor.py:247-265)
+__device__ void features(const BParams& p, int i, double ax, double ay, double gx, double gy, const int32_t* so) {
+  float f[20];
+#pragma unroll
+  for (int k = 0; k < 20; ++k) f[k] = 0.f;
+  // calcDistanceFromGoal (:132-144): floor(hypot / 5), capped at 5
+  const double dg = floor(hypot(ax - gx, ay - gy) / 5.0);
+  f[0] = (float)(dg > 5.0 ? 5.0 : dg);
+  // relativeGoalPos (:146-166): angle between (0, 1) and (gx - ax, gy - ay)
+  const double vx = gx - ax, vy = gy - ay;
+  const double nv = sqrt(__dadd_rn(__dmul_rn(vx, vx), __dmul_rn(vy, vy)));
+  double c = nv > 0.0 ? vy / nv : 0.0;
+  c = c < -1.0 ? -1.0 : (c > 1.0 ? 1.0 : c);
+  const double ang = acos(c);
+  if (ang < PI / 4) f[1] = 1.f;
+  else if (ang > PI / 4 && ang < PI * 3 / 4) f[vx > 0 ? 2 : 4] = 1.f;
+  else f[3] = 1.f;
+  // density (:91-112), speed/orientation (:115-130), social forces (:170-193)
+  double sf = 0.0;
+  for (int k = 0; k < p.ns; ++k) {
+    const int32_t o = so[k];
+    const double ox = (double)sx(o), oy = (double)sy(o);
+    const double N = dist2(ox, oy, ax, ay) - p.r_agent - p.r_feature_obs;   // calcDistance
+    if (N < 1000.0) f[7] += 1.f;
+    if (N < 230.0) f[6] += 1.f;
+    if (N < 101.0) f[5] += 1.f;
+    f[8 + 3 * 1 + 0] += 1.f;                           // orientation bin 1, speed bin 0
+    const double fsoc = exp(-N / 10.0) * N * 1.5;      // a*exp(-N/b)*N*thrPart, a = 1, b = 10
+    if (fsoc > 1.0) sf += fsoc;                        // -> phi_SF[orientation bin 1]
+  }
+  f[17 + 1] = (float)sf;
+  float* row = p.features + (int64_t)i * 20;
+#pragma unroll
+  for (int k = 0; k < 20; ++k) row[k] = f[k];
+}
+
+// createBoard.reset for env i (ballenv_pygame.py:460-513)
+__device__ void reset_env(const BParams& p, int i, uint32_t episode, double& ax, double& ay, double& gx, double& gy,
+                          double& d0, double& total, int32_t* so) {
+  Draws dr{p.tape, p.tape_len, p.n, i, 0, (uint32_t)p.gid0 + (uint32_t)i, episode, p.seed, u4{0, 0, 0, 0}, 0,
+           p.status};
+  // generate_randomval(lower, upper) = lower + ranf * (upper - lower)
+  auto rv = [&](int lo, int hi) { return (double)lo + dr.ranf() * (double)(hi - lo); };
+  gx = rv(p.W - p.sgx, p.W);
+  gy = rv(p.H - p.sgy, p.H);
+  ax = rv(0, p.sax);
+  ay = rv(0, p.say);
+  d0 = dist2(gx, gy, ax, ay);                                    // state[2]: the first distance
+  int guard = 0;
+  while (dist2(gx, gy, ax, ay) < p.min_spawn) {
+    if (++guard > BOARD_REJECT_LIMIT) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+    ax = rv(0, p.sax);
+    ay = rv(0, p.say);
+  }
+  for (int k = 0; k < p.ns; ++k) {
+    int ox = 0, oy = 0;
+    for (int a = 0;; ++a) {
+      if (a > BOARD_REJECT_LIMIT) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+      ox = dr.randint(p.sox, p.W - p.sox);
+      oy = dr.randint(p.soy, p.H - p.soy);
+      // not check_overlap(obs, agent, thresh=15) and not check_overlap(obs, goal, thresh=5)
+      const bool ok_a = dist2((double)ox, (double)oy, ax, ay) - p.thr_agent > p.r_collide;
+      const bool ok_g = dist2((double)ox, (double)oy, gx, gy) - p.thr_goal > p.r_collide;
+      if (ok_a && ok_g) break;
+    }
+    so[k] = (int32_t)(((uint32_t)ox & 0xFFFFu) | ((uint32_t)oy << 16));
+  }
+  total = dist2(ax, ay, gx, gy);                                 // total_distance
+}
+
+__global__ __launch_bounds__(256) void board_kernel(BParams p) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.n) return;
+  int32_t so[BE_BOARD_MAX_STATIC];
+  for (int k = 0; k < p.ns; ++k) so[k] = p.statics[(int64_t)k * p.n + i];
+  double ax = p.agent[2 * (int64_t)i], ay = p.agent[2 * (int64_t)i + 1];
+  double gx = p.goal[2 * (int64_t)i], gy = p.goal[2 * (int64_t)i + 1];
+  if (p.mode == 2) { features(p, i, ax, ay, gx, gy, so); return; }
+  uint32_t episode = p.episode[i];
+  bool do_reset = p.mode == 1 && (!p.mask || p.mask[i]);
+  double total = p.total[i], ret = p.ep_return[i], dist = p.dist[i];
+  int32_t len = p.ep_len[i];
+  if (p.mode == 0) {
+    double dx = 0.0, dy = 0.0;
+    if (p.actions) {
+      int a = p.actions[i];
+      if (a >= p.num_actions) { atomicOr(p.status, BE_STATUS_BAD_ACTION); a = 0; }
+      dx = p.tables->actions[a][0]; dy = p.tables->actions[a][1];
+    } else {
+      dx = p.deltas[2 * (int64_t)i]; dy = p.deltas[2 * (int64_t)i + 1];
+    }
+    const double old = dist2(ax, ay, gx, gy);                    // self.old_dist (:652)
+    double nx = ax + dx, ny = ay + dy;
+    if (nx < 0) nx = 0;
+    if (nx > p.W) nx = p.W;
+    if (ny < 0) ny = 0;
+    if (ny > p.H) ny = p.H;
+    ax = nx; ay = ny;
+    dist = dist2(ax, ay, gx, gy);                                // state[2] (:668)
+    // calc_reward (:680-706)
+    double r;
+    bool done = false;
+    for (int k = 0; k < p.ns && !done; ++k)
+      done = !(dist2(ax, ay, (double)sx(so[k]), (double)sy(so[k])) > p.r_collide);
+    if (done) { r = -1.0; ret += -1.0; }
+    else if (dist < p.goal_thr) { done = true; r = 1.0; ret += 1.0; }
+    else { r = (old - dist) / total; ret += r; }
+    ++len;
+    const bool trunc = !done && p.time_limit > 0 && len >= p.time_limit;
+    done = done || trunc;
+    p.reward[i] = r;
+    p.done[i] = done ? 1 : 0;
+    if (p.truncated) p.truncated[i] = trunc ? 1 : 0;
+    do_reset = done && p.autoreset;
+  }
+  if (do_reset) {
+    ++episode;
+    reset_env(p, i, episode, ax, ay, gx, gy, dist, total, so);
+    ret = 0.0; len = 0;
+    for (int k = 0; k < p.ns; ++k) p.statics[(int64_t)k * p.n + i] = so[k];
+    p.goal[2 * (int64_t)i] = gx; p.goal[2 * (int64_t)i + 1] = gy;
+    p.total[i] = total;
+    p.episode[i] = episode;
+  }
+  p.agent[2 * (int64_t)i] = ax; p.agent[2 * (int64_t)i + 1] = ay;
+  p.dist[i] = dist;
+  p.ep_return[i] = ret;
+  p.ep_len[i] = len;
+  if (p.features) features(p, i, ax, ay, gx, gy, so);
+}
+
+}  // namespace
+
+struct be_board {
+  be_board_config cfg;
+  int device;
+  int* status;
+  BoardTables* d_tables;
+  char err[512];
+};
+
+static thread_local char g_board_err[512];
+
+static int bfail(be_board* b, int code, const char* msg) {
+  snprintf(b ? b->err : g_board_err, 512, "%s", msg);
+  return code;
+}
+
+static int bhip(be_board* b, hipError_t e) {
+  char buf[256];
+  snprintf(buf, sizeof buf, "HIP error: %s", hipGetErrorString(e));
+  return bfail(b, BE_E_HIP, buf);
+}
+
+extern "C" {
+
+int be_board_config_default(be_board_config* c, int32_t num_envs, int32_t num_static) {
+  if (!c) return bfail(nullptr, BE_E_INVALID, "cfg is NULL");
+  memset(c, 0, sizeof *c);
+  c->num_envs = num_envs; c->num_static = num_static; c->seed = 0xB0A2Dull;
+  c->screen_width = 100; c->screen_height = 100;                       // ballenv_pygame.py:8-15
+  c->strip_obs_x = 0; c->strip_obs_y = 0; c->strip_goal_x = 100; c->strip_goal_y = 100;
+  c->strip_agent_x = 100; c->strip_agent_y = 100;
+  c->agent_radius = 10.0; c->static_radius = 10.0; c->obstacle_feature_radius = 20.0;   // :316, Obstacle rad :35-38
+  c->goal_threshold = 15.0; c->min_spawn_dist = 50.0; c->spawn_thresh_agent = 15.0; c->spawn_thresh_goal = 5.0;
+  static const double acts[4][2] = {{0, -1}, {1, 0}, {0, 1}, {-1, 0}};   // actionArray :352-353
+  c->num_actions = 4;
+  for (int a = 0; a < 4; ++a) { c->actions[a][0] = acts[a][0]; c->actions[a][1] = acts[a][1]; }
+  c->time_limit = 0; c->autoreset = 0;
+  return BE_OK;
+}
+
+int be_board_create(const be_board_config* cfg, int32_t device, be_board** out) {
+  if (!cfg || !out) return bfail(nullptr, BE_E_INVALID, "bad arguments to be_board_create");
+  *out = nullptr;
+  if (cfg->num_envs < 1) return bfail(nullptr, BE_E_INVALID, "num_envs must be >= 1");
+  if (cfg->num_static < 0 || cfg->num_static > BE_BOARD_MAX_STATIC)
+    return bfail(nullptr, BE_E_INVALID, "num_static must be in [0, 32]");
+  if (cfg->num_actions < 1 || cfg->num_actions > BE_BOARD_MAX_ACTIONS)
+    return bfail(nullptr, BE_E_INVALID, "num_actions must be in [1, 16]");
+  if (cfg->screen_width < 1 || cfg->screen_height < 1 || cfg->screen_width > 16384 || cfg->screen_height > 16384 ||
+      cfg->screen_width - 2 * cfg->strip_obs_x < 1 || cfg->screen_height - 2 * cfg->strip_obs_y < 1)
+    return bfail(nullptr, BE_E_INVALID, "screen / obstacle strips give an empty randint range");
+  if (cfg->env_offset < 0 || cfg->env_offset + (int64_t)cfg->num_envs > (1ll << 32))
+    return bfail(nullptr, BE_E_INVALID, "global env ids must fit in 32 bits");
+  be_board* b = new (std::nothrow) be_board();
+  if (!b) return bfail(nullptr, BE_E_NOMEM, "out of host memory");
+  b->cfg = *cfg;
+  b->device = device;
+  BoardTables t;
+  memset(&t, 0, sizeof t);
+  for (int a = 0; a < cfg->num_actions; ++a) { t.actions[a][0] = cfg->actions[a][0]; t.actions[a][1] = cfg->actions[a][1]; }
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc(&b->status, sizeof(int));
+  if (e == hipSuccess) e = hipMemset(b->status, 0, sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&b->d_tables, sizeof t);
+  if (e == hipSuccess) e = hipMemcpy(b->d_tables, &t, sizeof t, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    const int rc = bhip(nullptr, e);
+    if (b->status) (void)hipFree(b->status);
+    if (b->d_tables) (void)hipFree(b->d_tables);
+    delete b;
+    return rc;
+  }
+  *out = b;
+  return BE_OK;
+}
+
+int be_board_destroy(be_board* b) {
+  if (!b) return BE_OK;
+  if (b->status) (void)hipFree(b->status);
+  if (b->d_tables) (void)hipFree(b->d_tables);
+  delete b;
+  return BE_OK;
+}
+
+const char* be_board_last_error(const be_board* b) { return b ? b->err : g_board_err; }
+
+static int board_launch(be_board* b, const be_board_state* st, const be_board_out* out, int mode,
+                        const uint8_t* actions, const double* deltas, const uint8_t* mask, const double* tape,
+                        int32_t tape_len, void* stream) {
+  if (!b) return bfail(nullptr, BE_E_INVALID, "board is NULL");
+  if (!st || !st->agent || !st->goal || !st->dist || !st->total_dist || !st->ep_return || !st->ep_len ||
+      !st->episode || (b->cfg.num_static > 0 && !st->static_obs))
+    return bfail(b, BE_E_INVALID, "be_board_state has a NULL pointer");
+  if (!out) return bfail(b, BE_E_INVALID, "out is NULL");
+  if (mode == 0 && (!out->reward || !out->done)) return bfail(b, BE_E_INVALID, "be_board_step needs out->reward and out->done");
+  if (mode == 0 && !actions && !deltas) return bfail(b, BE_E_INVALID, "be_board_step needs actions or deltas");
+  if (mode == 2 && !out->features) return bfail(b, BE_E_INVALID, "be_board_observe needs out->features");
+  if (tape && tape_len < 0) return bfail(b, BE_E_INVALID, "tape_len < 0");
+  int cur = -1;
+  hipError_t e = hipGetDevice(&cur);
+  if (e == hipSuccess && cur != b->device) e = hipSetDevice(b->device);
+  if (e != hipSuccess) return bhip(b, e);
+  const be_board_config& c = b->cfg;
+  BParams p;
+  memset(&p, 0, sizeof p);
+  p.agent = st->agent; p.goal = st->goal; p.dist = st->dist; p.total = st->total_dist; p.ep_return = st->ep_return;
+  p.ep_len = st->ep_len; p.episode = st->episode; p.statics = st->static_obs;
+  p.features = out->features; p.reward = out->reward; p.done = out->done; p.truncated = out->truncated;
+  p.actions = actions; p.deltas = deltas; p.mask = mask; p.tape = tape; p.tape_len = tape ? tape_len : 0;
+  p.tables = b->d_tables; p.status = b->status; p.seed = c.seed;
+  p.n = c.num_envs; p.ns = c.num_static; p.num_actions = c.num_actions; p.time_limit = c.time_limit;
+  p.autoreset = c.autoreset; p.gid0 = (int32_t)(uint32_t)c.env_offset; p.mode = mode;
+  p.W = c.screen_width; p.H = c.screen_height; p.sox = c.strip_obs_x; p.soy = c.strip_obs_y;
+  p.sgx = c.strip_goal_x; p.sgy = c.strip_goal_y; p.sax = c.strip_agent_x; p.say = c.strip_agent_y;
+  p.r_collide = c.static_radius + c.agent_radius; p.r_feature_obs = c.obstacle_feature_radius;
+  p.r_agent = c.agent_radius; p.goal_thr = c.goal_threshold; p.min_spawn = c.min_spawn_dist;
+  p.thr_agent = c.spawn_thresh_agent; p.thr_goal = c.spawn_thresh_goal;
+  hipLaunchKernelGGL(board_kernel, dim3((unsigned)((c.num_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p);
+  e = hipGetLastError();
+  if (e != hipSuccess) return bhip(b, e);
+  return BE_OK;
+}
+
+int be_board_reset(be_board* b, const be_board_state* st, const uint8_t* mask, const double* reset_tape,
+                   int32_t tape_len, const be_board_out* out, void* stream) {
+  return board_launch(b, st, out, 1, nullptr, nullptr, mask, reset_tape, tape_len, stream);
+}
+
+int be_board_step(be_board* b, const be_board_state* st, const uint8_t* actions, const double* deltas,
+                  const be_board_out* out, void* stream) {
+  return board_launch(b, st, out, 0, actions, deltas, nullptr, nullptr, 0, stream);
+}
+
+int be_board_observe(be_board* b, const be_board_state* st, const be_board_out* out, void* stream) {
+  return board_launch(b, st, out, 2, nullptr, nullptr, nullptr, nullptr, 0, stream);
+}
+
+int be_board_status(be_board* b, int32_t* status_out, void* stream) {
+  if (!b || !status_out) return bfail(b, BE_E_INVALID, "bad arguments to be_board_status");
+  hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  int v = 0;
+  if (e == hipSuccess) e = hipMemcpy(&v, b->status, sizeof v, hipMemcpyDeviceToHost);
+  const int zero = 0;
+  if (e == hipSuccess) e = hipMemcpy(b->status, &zero, sizeof zero, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return bhip(b, e);
+  *status_out = v;
+  return BE_OK;
+}
+
+}  // extern "C"

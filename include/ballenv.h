@@ -221,6 +221,72 @@ int64_t be_policy_bytes(const be_policy* pol);
  * in its 20-px block of the 5x5 grid -- as u8 (out) and/or f32 (out_f32; NULL = skip). */
 int be_observe_blocks(be_ctx* ctx, const be_state* st, uint8_t* out, float* out_f32, void* stream);
 
+/* ---- the createBoard physics profile ----
+ * N independent ballenv_pygame.createBoard worlds (reset :460-513, step :650-675,
+ * calc_reward :680-706) with the 20 featureExtractor features (featureExtractor.py:247-265)
+ * that step() computes.  f64 coordinates (ranf spawns), static obstacles only (the
+ * reference's dynamic path is not runnable: createBoard never sets obstacle_goal_list). */
+#define BE_BOARD_MAX_STATIC 32
+#define BE_BOARD_MAX_ACTIONS 16
+#define BE_BOARD_FEATURES 20
+
+typedef struct be_board_config {
+  int32_t num_envs;
+  int32_t num_static;         /* createBoard(static_obstacles=) */
+  int64_t env_offset;         /* global id of local env 0 (Philox key) */
+  uint64_t seed;
+  int32_t screen_width, screen_height;                /* _screen_width/_height = 100 (:8-9) */
+  int32_t strip_obs_x, strip_obs_y;                   /* 0, 0 */
+  int32_t strip_goal_x, strip_goal_y;                 /* 100, 100 */
+  int32_t strip_agent_x, strip_agent_y;               /* 100, 100 */
+  double agent_radius;        /* agent_radius = 10 (:316) */
+  double static_radius;       /* static_obstacle_radius = 10: collisions at <= static + agent (:381-387) */
+  double obstacle_feature_radius;  /* Obstacle.rad = 20 (:35-38): featureExtractor's calcDistance */
+  double goal_threshold;      /* 15, strict < (:345, :690) */
+  double min_spawn_dist;      /* 50: agent re-sampled while closer to the goal (:476-481) */
+  double spawn_thresh_agent, spawn_thresh_goal;       /* 15, 5: static spawn rejection (:494) */
+  int32_t num_actions;
+  double actions[BE_BOARD_MAX_ACTIONS][2];            /* actionArray (:352-353): (0,-1),(1,0),(0,1),(-1,0) */
+  int32_t time_limit;         /* 0 = none (createBoard has no TimeLimit) */
+  int32_t autoreset;          /* 1: a done env is reset inside be_board_step */
+} be_board_config;
+
+typedef struct be_board_state {
+  double* agent;        /* (N, 2) f64  state[0] */
+  double* goal;         /* (N, 2) f64  state[1] */
+  double* dist;         /* (N) f64     state[2] */
+  double* total_dist;   /* (N) f64     total_distance */
+  double* ep_return;    /* (N) f64     total_reward_accumulated */
+  int32_t* ep_len;      /* (N) */
+  uint32_t* episode;    /* (N) resets so far (Philox key) */
+  int32_t* static_obs;  /* (Ns, N) int16x2 packed integer obstacle positions */
+} be_board_state;
+
+typedef struct be_board_out {
+  float* features;      /* (N, 20) f32 featureExtractor output (sensor_readings), or NULL */
+  double* reward;       /* (N) (step only) */
+  uint8_t* done;        /* (N) (step only) */
+  uint8_t* truncated;   /* (N) or NULL */
+} be_board_out;
+
+typedef struct be_board be_board;
+
+int be_board_config_default(be_board_config* cfg, int32_t num_envs, int32_t num_static);
+int be_board_create(const be_board_config* cfg, int32_t device, be_board** out);
+int be_board_destroy(be_board* b);
+const char* be_board_last_error(const be_board* b);
+/* createBoard.reset for every env (or mask[i] != 0).  reset_tape: (tape_len, N) f64, the
+ * reference's np.random.ranf / randint values in call order (parity); NULL: Philox. */
+int be_board_reset(be_board* b, const be_board_state* st, const uint8_t* mask, const double* reset_tape,
+                   int32_t tape_len, const be_board_out* out, void* stream);
+/* createBoard.step + featureExtractor for every env: actions (N) u8 indices into cfg.actions,
+ * or deltas (N, 2) f64 (take_action_from_user's float moves). */
+int be_board_step(be_board* b, const be_board_state* st, const uint8_t* actions, const double* deltas,
+                  const be_board_out* out, void* stream);
+/* featureExtractor of the current state (no state change). */
+int be_board_observe(be_board* b, const be_board_state* st, const be_board_out* out, void* stream);
+int be_board_status(be_board* b, int32_t* status_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

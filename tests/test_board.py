@@ -1,0 +1,150 @@
+"""The createBoard physics profile: ballenv_pygame.createBoard
+reset/step/calc_reward + featureExtractor, against golden vectors made by running the
+reference (tests/golden/make_golden_board.py) -- the C oracle on the CPU, and
+BatchedBoard (csrc/board.hip) on the GPU.
+
+Bar: positions, distances, rewards, returns and done bit-exact (f64, same operation
+order); features exact except the social-force sum f[18] (exp / hypot / acos are 1-ulp
+library functions on every side): |diff| <= 1e-5 * max(1, |f18|) in f32.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import load
+from oracle import oracle
+
+
+def cfg_for(n, ns):
+    import ctypes as C
+    from gym_ballenv_amd import _abi
+    c = _abi.BeBoardConfig()
+    _abi.lib().be_board_config_default(C.byref(c), n, ns)
+    return c
+
+
+def check_features(got, want, msg=""):
+    got, want = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    mask = np.ones(20, bool)
+    mask[18] = False
+    np.testing.assert_array_equal(got[..., mask], want[..., mask], err_msg=msg)
+    np.testing.assert_allclose(got[..., 18], want[..., 18], rtol=1e-5, atol=1e-5, err_msg=msg)
+
+
+def fixture(prefix):
+    fx = load("board")
+    return {k[len(prefix) + 1:]: v for k, v in fx.items() if k.startswith(prefix + "_")}
+
+
+@pytest.mark.parametrize("prefix", ["a", "b"])
+def test_oracle_board_golden(prefix):
+    g = fixture(prefix)
+    E, T = g["actions"].shape
+    ns = g["init_static"].shape[1]
+    cfg = cfg_for(E, ns)
+    st = oracle.board_new_state(cfg)
+    tape = g["reset_tape"].T[: int(g["reset_used"].max())]
+    status, f = oracle.board_reset(cfg, st, np.nan_to_num(tape))
+    assert status == 0
+    np.testing.assert_array_equal(st["agent"], g["init_agent"])
+    np.testing.assert_array_equal(st["goal"], g["init_goal"])
+    np.testing.assert_array_equal(st["dist"], g["init_dist"])
+    np.testing.assert_array_equal(st["total_dist"], g["init_total"])
+    np.testing.assert_array_equal(st["static_obs"].transpose(1, 0, 2), g["init_static"])
+    check_features(f, g["init_feat"], "reset")
+    for t in range(T):
+        r, d, f = oracle.board_step(cfg, st, actions=g["actions"][:, t])
+        np.testing.assert_array_equal(r, g["reward"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(d, g["done"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(st["agent"], g["agent"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(st["dist"], g["dist"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(st["ep_return"], g["ep_return"][:, t], err_msg=f"t={t}")
+        check_features(f, g["feat"][:, t], f"t={t}")
+
+
+def make_board(gpu, n, ns, **kw):
+    from gym_ballenv_amd import BatchedBoard
+    return BatchedBoard(n, ns, device=gpu, **kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prefix", ["a", "b"])
+def test_gpu_board_golden(gpu, prefix):
+    g = fixture(prefix)
+    E, T = g["actions"].shape
+    ns = g["init_static"].shape[1]
+    b = make_board(gpu, E, ns)
+    tape = torch.from_numpy(np.ascontiguousarray(np.nan_to_num(g["reset_tape"].T[: int(g["reset_used"].max())])))
+    f = b.reset(reset_tape=tape)
+    b.status()
+    np.testing.assert_array_equal(b.agent.cpu().numpy(), g["init_agent"])
+    np.testing.assert_array_equal(b.goal.cpu().numpy(), g["init_goal"])
+    np.testing.assert_array_equal(b.dist.cpu().numpy(), g["init_dist"])
+    np.testing.assert_array_equal(b.total_dist.cpu().numpy(), g["init_total"])
+    np.testing.assert_array_equal(b.static_obs.cpu().numpy().transpose(1, 0, 2), g["init_static"])
+    check_features(f.cpu().numpy(), g["init_feat"], "reset")
+    acts = torch.from_numpy(g["actions"]).to(gpu)
+    for t in range(T):
+        f, r, d, _ = b.step(acts[:, t])
+        np.testing.assert_array_equal(r.cpu().numpy(), g["reward"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(d.cpu().numpy(), g["done"][:, t].astype(bool), err_msg=f"t={t}")
+        np.testing.assert_array_equal(b.agent.cpu().numpy(), g["agent"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(b.ep_return.cpu().numpy(), g["ep_return"][:, t], err_msg=f"t={t}")
+        check_features(f.cpu().numpy(), g["feat"][:, t], f"t={t}")
+    b.status()
+    b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_board_philox_vs_oracle(gpu):
+    """Philox resets honour the reference's spawn rules; then float-delta and index steps
+    from those states are bit-exact against the oracle (N not a multiple of 256)."""
+    N, ns = 5000, 8
+    b = make_board(gpu, N, ns, seed=9)
+    b.reset()
+    b.status()
+    ag, go = b.agent.cpu().numpy(), b.goal.cpu().numpy()
+    so = b.static_obs.cpu().numpy().astype(np.float64)
+    assert (np.hypot(*(ag - go).T) >= 50).all()
+    assert ((0 <= ag) & (ag < 100)).all() and ((0 <= go) & (go < 100)).all()
+    for k in range(ns):
+        assert (np.sqrt(((so[k] - ag) ** 2).sum(1)) - 15 > 20).all()
+        assert (np.sqrt(((so[k] - go) ** 2).sum(1)) - 5 > 20).all()
+    cfg = cfg_for(N, ns)
+    st = {k: getattr(b, k).cpu().numpy().copy() for k in b.STATE_KEYS}
+    st["episode"] = st["episode"].view(np.uint32)
+    rng = np.random.default_rng(3)
+    for t in range(30):
+        if t % 2:
+            a = rng.integers(0, 4, N).astype(np.uint8)
+            f, r, d, _ = b.step(torch.from_numpy(a))
+            wr, wd, wf = oracle.board_step(cfg, st, actions=a)
+        else:
+            dl = rng.normal(0, 3, (N, 2))
+            f, r, d, _ = b.step(deltas=torch.from_numpy(dl))
+            wr, wd, wf = oracle.board_step(cfg, st, deltas=dl)
+        np.testing.assert_array_equal(r.cpu().numpy(), wr, err_msg=f"t={t}")
+        np.testing.assert_array_equal(d.cpu().numpy(), wd.astype(bool))
+        np.testing.assert_array_equal(b.agent.cpu().numpy(), st["agent"])
+        check_features(f.cpu().numpy(), wf, f"t={t}")
+    b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_board_autoreset_and_observe(gpu):
+    N = 2048
+    b = make_board(gpu, N, 6, seed=1, autoreset=True, time_limit=40)
+    b.reset()
+    ep0 = b.episode.clone()
+    acts = torch.randint(0, 4, (60, N), dtype=torch.uint8, device=gpu)
+    finished = torch.zeros(N, dtype=torch.bool, device=gpu)
+    for t in range(60):
+        _, _, d, info = b.step(acts[t])
+        finished |= d
+        assert bool((b.ep_len[d] == 0).all())
+    assert bool(finished.all())              # every env hit, reached the goal or timed out
+    assert bool((b.episode > ep0).all())
+    f1 = b.features.clone()
+    assert torch.equal(b.observe(), f1)      # observe() == the features step() wrote
+    b.status()
+    b.close()
