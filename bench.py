@@ -55,6 +55,8 @@ def parse():
                    help="config 5 leg: timed steps of the on-GPU policy rollout (0 = skip)")
     p.add_argument("--torch-policy-steps", type=int, default=50,
                    help="config 5 comparison: timed steps with the PyTorch-ROCm policy (0 = skip)")
+    p.add_argument("--board-steps", type=int, default=200,
+                   help="createBoard profile leg (SURVEY 8(f) rank 2): timed steps (0 = skip)")
     return p.parse_args()
 
 
@@ -165,6 +167,39 @@ def policy_leg(args, gb, dev, rank, world, stream):
     return res
 
 
+def board_leg(args, gb, dev, rank, world, stream):
+    """createBoard profile (ballenv_pygame.py:314-706 + featureExtractor): step + 20 features
+    for every env, random actionArray moves, 6 static obstacles, autoreset, graph replay."""
+    import ctypes as C
+    import torch
+    N, T = args.envs, args.board_steps
+    b = gb.BatchedBoard(N, 6, device=dev, seed=0xB0A2D, env_offset=rank * N, autoreset=True, time_limit=1000)
+    b.reset()
+    acts = torch.randint(0, 4, (T, N), dtype=torch.uint8, device=dev)
+    lib = b._lib
+    for t in range(10):
+        b.step(acts[t])
+    g = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(dev)
+    with torch.cuda.graph(g, stream=cap):
+        sp = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        for t in range(T):
+            lib.be_board_step(b._h, C.byref(b._st), C.c_void_p(acts[t].data_ptr()), None, C.byref(b._out), sp)
+    g.replay()
+    el, ms = timed_graph_steps([g], T, dev, stream, world)
+    b.status()
+    # bytes per env-step: agent/dist/ret/len R+W 44, goal/total/episode R 28, 6 statics R 24,
+    # action R 1, reward W 8, done+truncated W 2, features W 80
+    B = 44 + 28 + 4 * 6 + 1 + 10 + 80
+    res = {"workload": f"createBoard profile: step + featureExtractor (20 f32), {N} envs/GPU, 6 static obstacles, "
+                       "random actionArray moves, autoreset, hipGraph replay",
+           "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
+           "kernel_us_mean": ms * 1e3, "bytes_per_env_step": B, "achieved_GBs": B * N / (ms * 1e-3) / 1e9}
+    del g
+    b.close()
+    return res
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -270,6 +305,7 @@ def main():
             traffic, traffic_src = d.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT)
 
     pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
+    board_res = board_leg(args, gb, dev, rank, world, stream) if args.board_steps > 0 else None
 
     if rank == 0:
         line = {
@@ -291,6 +327,7 @@ def main():
             "cpu_baseline": base,
             "episodes": ep,
             "policy_rollout": pol_res,
+            "board_profile": board_res,
         }
         print(json.dumps(line), flush=True)
     env.close()
