@@ -138,7 +138,7 @@ struct PParams {
   int32_t n, F, A, gid0;
   int32_t img_bytes;
   int32_t dbg;               // BALLENV_POLICY_DEBUG ablation bits (timing only): 1 no staging, 2 no MFMA,
-                             // 4 no head FMAs, 8 no epilogue
+                             // 4 no head FMAs, 8 no epilogue, 16 exit at entry
 };
 
 // 16 obs bytes of env `env` starting at column c (zero beyond F / beyond N).
@@ -184,6 +184,7 @@ __global__ __launch_bounds__(POL_THREADS) void policy_kernel(PParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int blk0 = blockIdx.x * POL_ENVS;
   const int tile0 = blk0 + wave * 16;                 // this wave's 16-env column tile
+  if (p.dbg & 16) return;                             // ablation: launch cost alone
 
   // obs fragments (B operand), issued before the staging barrier
   v4i B[KS];
