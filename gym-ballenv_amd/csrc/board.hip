@@ -103,7 +103,8 @@ struct Draws {
 };
 
 // featureExtractor(state, obstacle_list, (0, 0), agent_rad) -> 20 f32 (featureExtractor.py:247-265)
-__device__ void features(const BParams& p, int i, double ax, double ay, double gx, double gy, const int32_t* so) {
+template <int MAXS>
+__device__ void features(const BParams& p, int i, double ax, double ay, double gx, double gy, const int32_t (&so)[MAXS]) {
   float f[20];
 #pragma unroll
   for (int k = 0; k < 20; ++k) f[k] = 0.f;
@@ -117,11 +118,13 @@ __device__ void features(const BParams& p, int i, double ax, double ay, double g
   c = c < -1.0 ? -1.0 : (c > 1.0 ? 1.0 : c);
   const double ang = acos(c);
   if (ang < PI / 4) f[1] = 1.f;
-  else if (ang > PI / 4 && ang < PI * 3 / 4) f[vx > 0 ? 2 : 4] = 1.f;
+  else if (ang > PI / 4 && ang < PI * 3 / 4) { if (vx > 0) f[2] = 1.f; else f[4] = 1.f; }
   else f[3] = 1.f;
   // density (:91-112), speed/orientation (:115-130), social forces (:170-193)
   double sf = 0.0;
-  for (int k = 0; k < p.ns; ++k) {
+#pragma unroll
+  for (int k = 0; k < MAXS; ++k) {
+    if (k >= p.ns) break;
     const int32_t o = so[k];
     const double ox = (double)sx(o), oy = (double)sy(o);
     const double N = dist2(ox, oy, ax, ay) - p.r_agent - p.r_feature_obs;   // calcDistance
@@ -133,14 +136,15 @@ __device__ void features(const BParams& p, int i, double ax, double ay, double g
     if (fsoc > 1.0) sf += fsoc;                        // -> phi_SF[orientation bin 1]
   }
   f[17 + 1] = (float)sf;
-  float* row = p.features + (int64_t)i * 20;
+  float4* row = reinterpret_cast<float4*>(p.features + (int64_t)i * 20);   // 80-B rows: 5 x 16 B
 #pragma unroll
-  for (int k = 0; k < 20; ++k) row[k] = f[k];
+  for (int k = 0; k < 5; ++k) row[k] = make_float4(f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
 }
 
 // createBoard.reset for env i (ballenv_pygame.py:460-513)
+template <int MAXS>
 __device__ void reset_env(const BParams& p, int i, uint32_t episode, double& ax, double& ay, double& gx, double& gy,
-                          double& d0, double& total, int32_t* so) {
+                          double& d0, double& total, int32_t (&so)[MAXS]) {
   Draws dr{p.tape, p.tape_len, p.n, i, 0, (uint32_t)p.gid0 + (uint32_t)i, episode, p.seed, u4{0, 0, 0, 0}, 0,
            p.status};
   // generate_randomval(lower, upper) = lower + ranf * (upper - lower)
@@ -156,7 +160,9 @@ __device__ void reset_env(const BParams& p, int i, uint32_t episode, double& ax,
     ax = rv(0, p.sax);
     ay = rv(0, p.say);
   }
-  for (int k = 0; k < p.ns; ++k) {
+#pragma unroll
+  for (int k = 0; k < MAXS; ++k) {
+    if (k >= p.ns) break;
     int ox = 0, oy = 0;
     for (int a = 0;; ++a) {
       if (a > BOARD_REJECT_LIMIT) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
@@ -172,13 +178,18 @@ __device__ void reset_env(const BParams& p, int i, uint32_t episode, double& ax,
   total = dist2(ax, ay, gx, gy);                                 // total_distance
 }
 
+// MAXS: compile-time bound on the static-obstacle count (8 / 16 / 32), so the obstacle
+// loops unroll with a runtime guard and the positions stay in registers (no scratch).
+template <int MAXS>
 __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= p.n) return;
-  int32_t so[BE_BOARD_MAX_STATIC];
-  for (int k = 0; k < p.ns; ++k) so[k] = p.statics[(int64_t)k * p.n + i];
-  double ax = p.agent[2 * (int64_t)i], ay = p.agent[2 * (int64_t)i + 1];
-  double gx = p.goal[2 * (int64_t)i], gy = p.goal[2 * (int64_t)i + 1];
+  int32_t so[MAXS];
+#pragma unroll
+  for (int k = 0; k < MAXS; ++k) so[k] = k < p.ns ? p.statics[(int64_t)k * p.n + i] : 0;
+  const double2 ag = reinterpret_cast<const double2*>(p.agent)[i];
+  const double2 gl = reinterpret_cast<const double2*>(p.goal)[i];
+  double ax = ag.x, ay = ag.y, gx = gl.x, gy = gl.y;
   if (p.mode == 2) { features(p, i, ax, ay, gx, gy, so); return; }
   uint32_t episode = p.episode[i];
   bool do_reset = p.mode == 1 && (!p.mask || p.mask[i]);
@@ -204,8 +215,9 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     // calc_reward (:680-706)
     double r;
     bool done = false;
-    for (int k = 0; k < p.ns && !done; ++k)
-      done = !(dist2(ax, ay, (double)sx(so[k]), (double)sy(so[k])) > p.r_collide);
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k)   // any hit (the reference stops at the first; the result is the same)
+      done = done || (k < p.ns && !(dist2(ax, ay, (double)sx(so[k]), (double)sy(so[k])) > p.r_collide));
     if (done) { r = -1.0; ret += -1.0; }
     else if (dist < p.goal_thr) { done = true; r = 1.0; ret += 1.0; }
     else { r = (old - dist) / total; ret += r; }
@@ -221,12 +233,14 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     ++episode;
     reset_env(p, i, episode, ax, ay, gx, gy, dist, total, so);
     ret = 0.0; len = 0;
-    for (int k = 0; k < p.ns; ++k) p.statics[(int64_t)k * p.n + i] = so[k];
-    p.goal[2 * (int64_t)i] = gx; p.goal[2 * (int64_t)i + 1] = gy;
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k)
+      if (k < p.ns) p.statics[(int64_t)k * p.n + i] = so[k];
+    reinterpret_cast<double2*>(p.goal)[i] = make_double2(gx, gy);
     p.total[i] = total;
     p.episode[i] = episode;
   }
-  p.agent[2 * (int64_t)i] = ax; p.agent[2 * (int64_t)i + 1] = ay;
+  reinterpret_cast<double2*>(p.agent)[i] = make_double2(ax, ay);
   p.dist[i] = dist;
   p.ep_return[i] = ret;
   p.ep_len[i] = len;
@@ -351,7 +365,8 @@ static int board_launch(be_board* b, const be_board_state* st, const be_board_ou
   p.r_collide = c.static_radius + c.agent_radius; p.r_feature_obs = c.obstacle_feature_radius;
   p.r_agent = c.agent_radius; p.goal_thr = c.goal_threshold; p.min_spawn = c.min_spawn_dist;
   p.thr_agent = c.spawn_thresh_agent; p.thr_goal = c.spawn_thresh_goal;
-  hipLaunchKernelGGL(board_kernel, dim3((unsigned)((c.num_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p);
+  void (*fn)(BParams) = c.num_static <= 8 ? board_kernel<8> : (c.num_static <= 16 ? board_kernel<16> : board_kernel<32>);
+  hipLaunchKernelGGL(fn, dim3((unsigned)((c.num_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p);
   e = hipGetLastError();
   if (e != hipSuccess) return bhip(b, e);
   return BE_OK;
