@@ -43,6 +43,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "ballenv.h"
 #include "internal.h"
@@ -61,7 +62,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 // Packed-weight image (bytes), identical in HBM and in each workgroup's LDS.
 struct PolLayout {
   int HT, KS, NO;            // 16-row hidden tiles, 64-wide K steps, outputs (actions + value)
-  int frag, bias, head, hbias, total, logits, lds;
+  int frag, bias, head, hbias, table, total, logits, info, list, count, lds;
 };
 __host__ __device__ constexpr PolLayout pol_layout(int HT, int KS, int NO) {
   PolLayout L{};
@@ -70,9 +71,13 @@ __host__ __device__ constexpr PolLayout pol_layout(int HT, int KS, int NO) {
   L.bias = L.frag + HT * 3 * KS * 1024;         // [HT*16] i32   bq_k = rint(b1_k / s_k)
   L.head = L.bias + HT * 16 * 4;                // [HT][4 groups][NO][4] f32  W_o,k * s_k, k = 16ht+4g+r
   L.hbias = L.head + HT * 4 * NO * 4 * 4;       // [NO] f32 (pad actions: -inf; value last)
-  L.total = (L.hbias + NO * 4 + 15) & ~15;
+  L.table = L.hbias + NO * 4;                   // [4][NO] f32 raw logits of the obs e_0..e_3 (empty window)
+  L.total = (L.table + 4 * NO * 4 + 15) & ~15;
   L.logits = L.total;                           // LDS only: [POL_ENVS][NO] f32 for the epilogue
-  L.lds = L.logits + POL_ENVS * NO * 4;
+  L.info = L.logits + POL_ENVS * NO * 4;        // LDS only: [POL_ENVS] u8
+  L.list = L.info + POL_ENVS;                   // LDS only: [POL_ENVS] i16 envs with a lit window cell
+  L.count = L.list + POL_ENVS * 2;              // LDS only: i32
+  L.lds = L.count + 16;
   return L;
 }
 
@@ -134,11 +139,12 @@ struct PParams {
   float* log_prob;           // (N) or NULL
   float* value;              // (N) or NULL
   float* probs;              // (N, A) or NULL
+  float* table_out;          // table mode: (N, NO) raw logits, every env dense, no draw
   unsigned long long seed;
   int32_t n, F, A, gid0;
   int32_t img_bytes;
   int32_t dbg;               // BALLENV_POLICY_DEBUG ablation bits (timing only): 1 no staging, 2 no MFMA,
-                             // 4 no head FMAs, 8 no epilogue, 16 exit at entry
+                             // 4 no head FMAs, 8 no epilogue, 16 exit at entry, 32 every env dense
 };
 
 // 16 obs bytes of env `env` starting at column c (zero beyond F / beyond N).
@@ -177,19 +183,83 @@ __device__ __forceinline__ float sum_groups(float x) {
 #define BE_POL_UNROLL 13
 #endif
 
+// OR of x over lanes l, l^16, l^32, l^48
+__device__ __forceinline__ uint32_t or_groups(uint32_t x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  x = a[0] | a[1];
+  const auto b = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return b[0] | b[1];
+}
+
+// The dense forward of one 16-env column tile (env of lane = lane & 15, obs fragments B):
+// fc1 on the int8 MFMA, relu, heads.  Returns the raw logits (before the head bias),
+// summed over the lane groups (every lane of a column holds its env's values).
+template <int HT, int KS, int NO>
+__device__ __forceinline__ void tile_forward(const uint8_t* lds, const v4i (&B)[KS], int lane, int dbg,
+                                             float (&out)[NO]) {
+  constexpr PolLayout L = pol_layout(HT, KS, NO);
+  const int g = lane >> 4;
+  float part[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) part[o] = 0.f;
+#pragma unroll BE_POL_UNROLL
+  for (int ht = 0; ht < HT; ++ht) {
+    v4i acc[3];   // one accumulator per digit plane: no VALU between a tile row's MFMAs
+    acc[0] = v4i{0, 0, 0, 0};
+    acc[1] = v4i{0, 0, 0, 0};
+    acc[2] = *(const v4i*)(lds + L.bias + (ht * 16 + 4 * g) * 4);
+    if (!(dbg & 2)) {
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const v4i a = *(const v4i*)(lds + L.frag + ((((ht * 3 + d) * KS + ks) * 64 + lane) << 4));
+          acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, B[ks], acc[d], 0, 0, 0);
+        }
+    } else {
+      acc[2] += B[0];
+    }
+    float h[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = (int)(((uint32_t)acc[0][r] << 16) + ((uint32_t)acc[1][r] << 8)) + acc[2][r];
+      h[r] = (float)(q > 0 ? q : 0);
+    }
+    if (!(dbg & 4)) {
+#pragma unroll
+      for (int o = 0; o < NO; ++o) {
+        const float4 w = *(const float4*)(lds + L.head + (((ht * 4 + g) * NO + o) * 4) * 4);
+        part[o] = fmaf(w.w, h[3], fmaf(w.z, h[2], fmaf(w.y, h[1], fmaf(w.x, h[0], part[o]))));
+      }
+    } else {
+      part[0] += h[0] + h[1] + h[2] + h[3];
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < NO; ++o) out[o] = sum_groups(part[o]);
+}
+
+// Sparse structure of the input: an env whose window has no lit cell has the obs e_q (its
+// quadrant one-hot) -- over 90 % of envs in rollouts (0.7 % of obs have a lit cell under
+// random actions, 7.6 % under the reference's trained Policy(10)).  Their logits are the
+// 4-entry table the pack step computes by running tile_forward on the obs e_0..e_3, so they
+// are bit-identical to the dense result.  Each workgroup compacts its envs with a lit cell
+// into a list in LDS and only those go through the matrix cores, in 16-env tiles.
+// p.table_out != NULL: "table mode" -- every env dense, raw logits to table_out (no draw).
 template <int HT, int KS, int NO, bool ALIGNED8>
 __global__ __launch_bounds__(POL_THREADS) void policy_kernel(PParams p) {
   extern __shared__ uint4 pol_lds[];
   constexpr PolLayout L = pol_layout(HT, KS, NO);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int blk0 = blockIdx.x * POL_ENVS;
-  const int tile0 = blk0 + wave * 16;                 // this wave's 16-env column tile
+  const int tile0 = blk0 + wave * 16;                 // this wave's 16 envs for the scan
   if (p.dbg & 16) return;                             // ablation: launch cost alone
-
-  // obs fragments (B operand), issued before the staging barrier
-  v4i B[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) B[ks] = load_obs16<ALIGNED8>(p, tile0 + (lane & 15), 64 * ks + 16 * g);
+  uint8_t* lds = (uint8_t*)pol_lds;
+  uint8_t* info = lds + L.info;                       // per env: bit 7 = a lit cell, bits 0-1 = quadrant
+  int16_t* list = (int16_t*)(lds + L.list);
+  int* count = (int*)(lds + L.count);
+  const bool dense = p.table_out != nullptr || (p.dbg & 32);
+  if (tid == 0) *count = 0;
 
   // the epilogue's Philox key words, prefetched (lane l of wave w < 4 finishes env blk0 + 64w + l)
   const int e_loc = wave * 64 + lane, my_env = blk0 + e_loc;
@@ -197,70 +267,63 @@ __global__ __launch_bounds__(POL_THREADS) void policy_kernel(PParams p) {
   const uint32_t episode = fin ? p.episode[my_env] : 0u;
   const int32_t len = fin ? p.ep_len[my_env] : 0;
 
-  if (!(p.dbg & 1)) {  // stage the packed weights
+  // scan: this wave's 16 envs, 16 obs bytes per lane and K step (the B-operand layout)
+  v4i B[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) B[ks] = load_obs16<ALIGNED8>(p, tile0 + (lane & 15), 64 * ks + 16 * g);
+  uint32_t lit = 0;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    lit |= ((ks == 0 && g == 0) ? 0u : (uint32_t)B[ks][0]) | (uint32_t)B[ks][1] | (uint32_t)B[ks][2] | (uint32_t)B[ks][3];
+  lit = or_groups(lit);
+  __syncthreads();   // *count = 0 is visible
+
+  if (!(p.dbg & 1)) {  // stage the packed weights (overlaps the scan's loads)
     const uint4* src = (const uint4*)p.img;
     const int n16 = p.img_bytes >> 4;
     for (int i = tid; i < n16; i += POL_THREADS) pol_lds[i] = src[i];
   }
-  __syncthreads();
+  if (g == 0 && tile0 + lane < p.n) {
+    // obs bytes 0..3 must be exactly a quadrant one-hot for the table (any other input is dense)
+    const uint32_t q4 = (uint32_t)B[0][0];
+    const int quad = q4 == 1u ? 0 : (q4 == 0x100u ? 1 : (q4 == 0x10000u ? 2 : 3));
+    const bool onehot = q4 == 1u || q4 == 0x100u || q4 == 0x10000u || q4 == 0x1000000u;
+    const bool nz = dense || lit != 0u || !onehot;
+    info[wave * 16 + lane] = (uint8_t)(quad | (nz ? 0x80 : 0));
+    if (nz) list[atomicAdd(count, 1)] = (int16_t)(wave * 16 + lane);
+  }
+  __syncthreads();   // weights staged, list complete
 
-  uint8_t* lds = (uint8_t*)pol_lds;
-  float part[NO];
+  float* lg = (float*)(lds + L.logits);
+  const int cnt = *count;
+  if (wave * 16 < cnt) {
+    const int k = wave * 16 + (lane & 15);
+    const int e = k < cnt ? list[k] : -1;
+    v4i Bt[KS];
 #pragma unroll
-  for (int o = 0; o < NO; ++o) part[o] = 0.f;
-
-  if (tile0 < p.n) {
-#pragma unroll BE_POL_UNROLL
-    for (int ht = 0; ht < HT; ++ht) {
-      v4i acc[3];   // one accumulator per digit plane: no VALU between a tile row's MFMAs
-      acc[0] = v4i{0, 0, 0, 0};
-      acc[1] = v4i{0, 0, 0, 0};
-      acc[2] = *(const v4i*)(lds + L.bias + (ht * 16 + 4 * g) * 4);
-      if (!(p.dbg & 2)) {
+    for (int ks = 0; ks < KS; ++ks) Bt[ks] = load_obs16<ALIGNED8>(p, e >= 0 ? blk0 + e : p.n, 64 * ks + 16 * g);
+    float out[NO];
+    tile_forward<HT, KS, NO>(lds, Bt, lane, p.dbg, out);
+    if (g == 0 && e >= 0) {
 #pragma unroll
-        for (int d = 0; d < 3; ++d)
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) {
-            const v4i a = *(const v4i*)(lds + L.frag + ((((ht * 3 + d) * KS + ks) * 64 + lane) << 4));
-            acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, B[ks], acc[d], 0, 0, 0);
-          }
-      } else {
-        acc[2] += B[0];
-      }
-      float h[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = (int)(((uint32_t)acc[0][r] << 16) + ((uint32_t)acc[1][r] << 8)) + acc[2][r];
-        h[r] = (float)(q > 0 ? q : 0);
-      }
-      if (!(p.dbg & 4)) {
-#pragma unroll
-        for (int o = 0; o < NO; ++o) {
-          const float4 w = *(const float4*)(lds + L.head + (((ht * 4 + g) * NO + o) * 4) * 4);
-          part[o] = fmaf(w.w, h[3], fmaf(w.z, h[2], fmaf(w.y, h[1], fmaf(w.x, h[0], part[o]))));
-        }
-      } else {
-        part[0] += h[0] + h[1] + h[2] + h[3];
-      }
-    }
-    // sum over the 4 lane groups (hidden-unit quarters); group 0 publishes its env's logits
-    float* lg = (float*)(lds + L.logits);
-#pragma unroll
-    for (int o = 0; o < NO; ++o) {
-      const float x = sum_groups(part[o]);
-      if (g == 0) lg[(wave * 16 + lane) * NO + o] = x;
+      for (int o = 0; o < NO; ++o) lg[e * NO + o] = out[o];
     }
   }
   __syncthreads();
-  if (wave >= POL_FIN_WAVES || (p.dbg & 8)) return;
+  if (wave >= POL_FIN_WAVES || (p.dbg & 8) || !fin) return;
 
   // epilogue: lane l of wave w finishes env blk0 + 64w + l
-  if (!fin) return;
-  const float* lg = (const float*)(lds + L.logits) + e_loc * NO;
+  const uint8_t inf = info[e_loc];
+  const float* src = (inf & 0x80) ? lg + e_loc * NO : (const float*)(lds + L.table) + (inf & 3) * NO;
+  if (p.table_out) {
+#pragma unroll
+    for (int o = 0; o < NO; ++o) p.table_out[(int64_t)my_env * NO + o] = src[o];
+    return;
+  }
   const float* hb = (const float*)(lds + L.hbias);
   float logit[NO];
 #pragma unroll
-  for (int o = 0; o < NO; ++o) logit[o] = lg[o] + hb[o];
+  for (int o = 0; o < NO; ++o) logit[o] = src[o] + hb[o];
 
   // softmax over the action logits (pads are -inf), Categorical draw by inverse CDF
   float mx = logit[0];
@@ -331,6 +394,8 @@ struct be_policy {
   PolKernel k;
   PolLayout L;
   uint8_t* img;
+  uint8_t* obs4;     // (4, F) u8: the empty-window obs e_0..e_3 (table pass input)
+  uint32_t* zero4;   // (4) zero episode / ep_len words for the table pass
   bool loaded;
   int dbg;
 };
@@ -360,9 +425,20 @@ int be_policy_create(be_ctx* ctx, int32_t hidden, int32_t num_actions, be_policy
   hipError_t e = hipSuccess;
   if (rc == BE_OK) e = hipMalloc(&pol->img, (size_t)pol->L.total);
   if (rc == BE_OK && e == hipSuccess) e = hipMemset(pol->img, 0, (size_t)pol->L.total);
+  if (rc == BE_OK && e == hipSuccess) e = hipMalloc(&pol->obs4, (size_t)4 * F);
+  if (rc == BE_OK && e == hipSuccess) e = hipMalloc(&pol->zero4, 4 * sizeof(uint32_t));
+  if (rc == BE_OK && e == hipSuccess) e = hipMemset(pol->zero4, 0, 4 * sizeof(uint32_t));
+  if (rc == BE_OK && e == hipSuccess) {
+    uint8_t h[4 * POL_MAXF];
+    memset(h, 0, sizeof h);
+    for (int q = 0; q < 4; ++q) h[q * F + q] = 1;
+    e = hipMemcpy(pol->obs4, h, (size_t)4 * F, hipMemcpyHostToDevice);
+  }
   if (rc == BE_OK && e != hipSuccess) rc = pol_hip_fail(ctx, e);
   if (rc != BE_OK) {
     if (pol->img) (void)hipFree(pol->img);
+    if (pol->obs4) (void)hipFree(pol->obs4);
+    if (pol->zero4) (void)hipFree(pol->zero4);
     delete pol;
     return rc;
   }
@@ -373,6 +449,8 @@ int be_policy_create(be_ctx* ctx, int32_t hidden, int32_t num_actions, be_policy
 int be_policy_destroy(be_policy* pol) {
   if (!pol) return BE_OK;
   if (pol->img) (void)hipFree(pol->img);
+  if (pol->obs4) (void)hipFree(pol->obs4);
+  if (pol->zero4) (void)hipFree(pol->zero4);
   delete pol;
   return BE_OK;
 }
@@ -387,6 +465,14 @@ int be_policy_load(be_policy* pol, const float* fc1_w, const float* fc1_b, const
   const PolPack a{fc1_w, fc1_b, act_w, act_b, val_w, val_b, pol->H, pol->F, pol->A};
   hipLaunchKernelGGL(policy_pack_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a, pol->img, pol->L);
   POL_TRY(ctx, hipGetLastError());
+  // table pass: the dense forward of the 4 empty-window obs, into the image's table
+  PParams p;
+  memset(&p, 0, sizeof p);
+  p.img = pol->img; p.obs = pol->obs4; p.episode = pol->zero4; p.ep_len = (const int32_t*)pol->zero4;
+  p.table_out = (float*)(pol->img + pol->L.table);
+  p.n = 4; p.F = pol->F; p.A = pol->A; p.img_bytes = pol->L.total;
+  hipLaunchKernelGGL(pol->k.fn, dim3(1), dim3(POL_THREADS), (size_t)pol->L.lds, (hipStream_t)stream, p);
+  POL_TRY(ctx, hipGetLastError());
   pol->loaded = true;
   return BE_OK;
 }
@@ -400,6 +486,7 @@ int be_policy_act(be_policy* pol, const be_state* st, const uint8_t* obs, const 
     return be_ctx_fail(ctx, BE_E_INVALID, "be_policy_act needs state episode/ep_len, obs and out->action");
   if (int rc = pol_set_device(ctx, pol->cv.device)) return rc;
   PParams p;
+  memset(&p, 0, sizeof p);
   p.img = pol->img; p.obs = obs; p.episode = st->episode; p.ep_len = st->ep_len;
   p.action = out->action; p.log_prob = out->log_prob; p.value = out->value; p.probs = out->probs;
   p.seed = (unsigned long long)seed; p.n = pol->cv.num_envs; p.F = pol->F; p.A = pol->A;

@@ -202,3 +202,33 @@ def test_a2c_update_on_gpu_rollout(gpu):
     a_new = check_act(env, pol.cpu(), hp2, env.obs, seed=9)
     assert torch.equal(ro.hp.act(seed=9)[0].cpu(), a_new)      # the rollout's kernel was re-packed
     hp2.close(); ro.close(); env.close()
+
+
+@pytest.mark.parametrize("W", [10, 5])
+def test_policy_sparse_path_equals_dense(gpu, W, monkeypatch):
+    """The empty-window fast path (table of the 4 quadrant-only obs + compacted lit envs) is
+    bit-identical to running every env through the matrix cores (BALLENV_POLICY_DEBUG=32)."""
+    from gym_ballenv_amd.policy import HipPolicy
+    env = make(gpu, 3000, W, seed=8)
+    acts = env.sample_actions(30, seed=4)
+    for t in range(30):
+        env.step(acts[t])
+    pol = ref_policy(W)
+    g = torch.Generator().manual_seed(1)
+    rand_obs = (torch.rand(3000, env.obs_dim, generator=g) < 0.05).to(torch.uint8)
+    rand_obs[:, :4] = 0
+    rand_obs[torch.arange(3000), torch.randint(0, 4, (3000,), generator=g)] = 1
+    hps = []
+    for dbg in ("0", "32"):
+        monkeypatch.setenv("BALLENV_POLICY_DEBUG", dbg)
+        hps.append(HipPolicy(env, pol, probs=True))
+    monkeypatch.delenv("BALLENV_POLICY_DEBUG")
+    lit = int((env.obs[:, 4:].sum(1) > 0).sum())
+    assert 0 < lit < 3000
+    for obs in (env.obs, rand_obs.to(gpu)):
+        r = [[x.clone() for x in hp.act(obs, seed=6)] for hp in hps]
+        for a, b in zip(*r):
+            assert torch.equal(a, b)
+    for hp in hps:
+        hp.close()
+    env.close()
