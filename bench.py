@@ -55,6 +55,12 @@ def parse():
                    help="config 5 leg: timed steps of the on-GPU policy rollout (0 = skip)")
     p.add_argument("--torch-policy-steps", type=int, default=50,
                    help="config 5 comparison: timed steps with the PyTorch-ROCm policy (0 = skip)")
+    p.add_argument("--rollout-steps", type=int, default=1000,
+                   help="fused be_rollout leg (SURVEY 8(d) fused multi-step mode): timed steps (0 = skip)")
+    p.add_argument("--rollout-chunk", type=int, default=100, help="steps per be_rollout launch")
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="N > 1 collective backend (nccl = RCCL over xGMI); gloo only to rehearse the "
+                        "multi-rank path with several ranks sharing one GPU")
     p.add_argument("--board-steps", type=int, default=200,
                    help="createBoard profile leg (SURVEY 8(f) rank 2): timed steps (0 = skip)")
     return p.parse_args()
@@ -167,6 +173,63 @@ def policy_leg(args, gb, dev, rank, world, stream):
     return res
 
 
+def rollout_leg(args, gb, dev, rank, world, stream):
+    """SURVEY 8(d) fused multi-step mode: the same random-action rollout as the headline, but
+    be_rollout runs --rollout-chunk steps per launch with each env's state in registers
+    (bit-identical outputs to be_step, tests/test_gpu_rollout.py).  Per step it writes the
+    obs row, reward, done and truncated of every env into (K, N, ...) trajectory buffers."""
+    import ctypes as C
+    import torch
+    from gym_ballenv_amd import _abi
+    N, W, T, Kc = args.envs, args.window, args.rollout_steps, max(1, min(args.rollout_chunk, args.rollout_steps))
+    T -= T % Kc
+    env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
+    acts = env.sample_actions(T, seed=0xBA11)
+    env.reset()
+    env.rollout(acts[:Kc])                    # warm-up launch; allocates the (Kc, N, ...) buffers
+    obs, rew, done, info = env.rollout(acts[:Kc])
+    out = _abi.BeOut(obs.data_ptr(), None, rew.data_ptr(), done.data_ptr(), info["truncated"].data_ptr(), None,
+                     info["final_return"].data_ptr(), info["final_len"].data_ptr(), env.stats_buf.data_ptr())
+    lib, ctx, st = env._lib, env._ctx, C.byref(env._st)
+    a0 = acts.data_ptr()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    sp = C.c_void_p(stream.cuda_stream)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for c0 in range(0, T, Kc):
+        rc = lib.be_rollout(ctx, st, C.c_void_p(a0 + c0 * N), Kc, C.byref(out), sp)
+        if rc:
+            _abi.check(rc, ctx)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    us_step = ev0.elapsed_time(ev1) * 1e3 / T
+    env.status()
+    # algorithmic bytes / env-step (SURVEY 8(d) fused mode): action 1 + reward 8 + done 1 + truncated 1
+    # + obs (4+W^2), plus the engine's state read+write (275 - 115 = 161 B at the defaults) once per launch
+    B_io = 1 + 8 + 1 + 1 + 4 + W * W
+    B_state = gb.step_bytes(gb.EnvConfig(), W) - (1 + 8 + 1 + 4 + W * W)
+    B = B_io + B_state / Kc
+    res = {"workload": f"random-action rollout, {N} envs/GPU, W={W}, be_rollout {Kc} steps per launch "
+                       "(state in registers; per-step obs/reward/done/truncated to (K, N, ...) buffers)",
+           "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
+           "kernel_us_per_step": us_step, "bytes_per_env_step": B,
+           "achieved_GBs": B * N / (us_step * 1e-6) / 1e9,
+           "frac": B * N / (us_step * 1e-6) / 1e9 / HBM_PEAK_GBS}
+    env.close()
+    return res
+
+
 def board_leg(args, gb, dev, rank, world, stream):
     """createBoard profile (ballenv_pygame.py:314-706 + featureExtractor): step + 20 features
     for every env, random actionArray moves, 6 static obstacles, autoreset, graph replay."""
@@ -215,10 +278,15 @@ def main():
     import gym_ballenv_amd as gb
     from gym_ballenv_amd import _abi
 
+    if args.dist_backend == "gloo":           # rehearsal: ranks may share a GPU
+        local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     N, W = args.envs, args.window
     cfg = gb.EnvConfig()
@@ -306,6 +374,7 @@ def main():
 
     pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
     board_res = board_leg(args, gb, dev, rank, world, stream) if args.board_steps > 0 else None
+    roll_res = rollout_leg(args, gb, dev, rank, world, stream) if args.rollout_steps > 0 else None
 
     if rank == 0:
         line = {
@@ -328,6 +397,7 @@ def main():
             "episodes": ep,
             "policy_rollout": pol_res,
             "board_profile": board_res,
+            "fused_rollout": roll_res,
         }
         print(json.dumps(line), flush=True)
     env.close()

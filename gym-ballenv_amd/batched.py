@@ -179,6 +179,39 @@ class BatchedBallEnv:
             info["terminal_obs"] = self.terminal_obs
         return (self.obs_f32 if self._want_f32 else self.obs), self.reward, self.done, info
 
+    def rollout(self, actions: torch.Tensor):
+        """``K = actions.shape[0]`` consecutive steps in one launch (be_rollout).
+
+        actions: (K, N) integer indices into ``cfg.actions``.  Returns per-step
+        ``(obs (K, N, F) u8, reward (K, N) f64, done (K, N) bool, info)`` with info
+        ``truncated`` / ``final_return`` / ``final_len`` (K, N) -- exactly what K calls of
+        :meth:`step` return, stacked (the reference's per-step loop of
+        examples/ball_cnn_ac3.py:573-600, for every env).  The state advances by K steps.
+        u8 obs only; the buffers are reused by the next rollout of the same K.
+        """
+        if self._want_f32 or self._want_terminal:
+            raise ValueError("rollout() returns u8 obs only (build the env without obs_f32 / terminal_obs)")
+        a = actions if actions.dtype == torch.uint8 else actions.to(torch.uint8)
+        if a.device != self.device:
+            a = a.to(self.device)
+        a = a.contiguous()
+        if a.dim() != 2 or a.shape[1] != self.num_envs:
+            raise ValueError(f"actions must be (K, {self.num_envs}), got {tuple(a.shape)}")
+        K, N, F = a.shape[0], self.num_envs, self.obs_dim
+        buf = getattr(self, "_ro_buf", None)
+        if buf is None or buf[0].shape[0] != K:
+            z = lambda *shape, dt: torch.zeros(*shape, dtype=dt, device=self.device)  # noqa: E731
+            buf = (z(K, N, F, dt=torch.uint8), z(K, N, dt=torch.float64), z(K, N, dt=torch.bool),
+                   z(K, N, dt=torch.bool), z(K, N, dt=torch.float64), z(K, N, dt=torch.int32))
+            self._ro_buf = buf
+        obs, reward, done, trunc, fret, flen = buf
+        out = _abi.BeOut(obs.data_ptr(), None, reward.data_ptr(), done.data_ptr(), trunc.data_ptr(), None,
+                         fret.data_ptr(), flen.data_ptr(), self.stats_buf.data_ptr() if self._track_stats else None)
+        _abi.check(self._lib.be_rollout(self._ctx, C.byref(self._st), a.data_ptr(), int(K), C.byref(out),
+                                        self._stream()), self._ctx)
+        self._keep = (a,)
+        return obs, reward, done, {"truncated": trunc, "final_return": fret, "final_len": flen}
+
     def observe(self) -> torch.Tensor:
         """prep_state4 of the current state (no state change)."""
         _abi.check(self._lib.be_observe(self._ctx, C.byref(self._st), C.byref(self._out), self._stream()), self._ctx)

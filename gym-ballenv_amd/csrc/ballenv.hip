@@ -100,6 +100,7 @@ struct KParams {
   // fixed-shape kernels only (pick_kernel checks the preconditions):
   uint32_t amx, amy;           // action a's (dx+1, dy+1) at bits 2a..2a+1 (every move in {-1,0,1})
   int32_t num_goals;           // goals pairwise distinct: newGoalList(g)[pick] = pick + (pick >= g)
+  int32_t steps;               // rollout_kernel: steps per launch (actions / outputs are (steps, N, ...))
 };
 
 // Diagnostic phase-skip bits (timing ablations only; outputs are wrong when set).  Only
@@ -694,20 +695,30 @@ __device__ void stage_full_row(uint8_t* dst, const uint32_t (&flat)[Geo<WT>::NW]
   }
 }
 
+// A reset env's distances: returns total_distance = |agent - goal| and sets prev to the
+// pre-resample distance (Q9; equal to total unless the agent was re-drawn).
+__device__ __forceinline__ double reset_dists(int32_t ag, int32_t go, int32_t a0, double& prev) {
+  const double td = calc_dist(px(ag), py(ag), px(go), py(go));
+  prev = a0 == ag ? td : calc_dist(px(go), py(go), px(a0), py(a0));
+  return td;
+}
+
 // Wave-cooperative autoreset (fixed-shape step kernels).  The finished envs of one wave are
 // reset by the whole wave, P = 64 / (NS+ND) envs per pass: lane s*(NS+ND) + k draws obstacle k
 // of the pass's env s (and, redundantly, that env's goal/agent) and ORs its window rows into a
 // per-wave LDS buffer, so no other wave of the block waits on them (no block barrier).  Draws
 // use reset_env_philox's counter layout, so results equal the block-cooperative path's.
-// wl: per-wave LDS scratch, >= P*(K+8) words.
-template <int WT, int NSC, int NDC, int PMAX>
+// wl: per-wave LDS scratch, >= P*(K+8) words.  Where the new state goes is the caller's:
+// osink(slot, k, il, packed xy) for obstacle k of env il (drawn by lane slot*G + k), then
+// esink(own, agent, goal, pre-resample agent) on the env's own lane, after a wave barrier.
+template <int WT, int NSC, int NDC, int PMAX, class OSink, class ESink>
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
-                            uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl) {
+                            uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl, OSink&& osink, ESink&& esink) {
   constexpr int K = Geo<WT>::K, G = NSC + NDC, P = (64 / G < PMAX) ? 64 / G : PMAX;
   static_assert(P >= 1, "one env's obstacles must fit a wave");
   const int lane = (int)(threadIdx.x & 63);
-  const int N = p.n, W = p.screen_w, H = p.screen_h;
+  const int W = p.screen_w, H = p.screen_h;
   const int rx = t.radius_obstacle + t.radius_agent, ry2 = t.radius_obstacle + 2 * t.radius_agent;
   const int slot = lane / G, k = lane - slot * G;
   uint32_t* wrows = wl;            // [P][K] row masks
@@ -764,11 +775,8 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
           ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
           oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
         }
-        (p.static_obs + (size_t)k * N)[il] = pk(ox, oy);
-      } else {
-        (p.dyn_obs + (size_t)(k - NSC) * N)[il] = pk(ox, oy);
-        (p.dyn_goal + (size_t)(k - NSC) * N)[il] = (uint8_t)(k - NSC);
       }
+      osink(slot, k, il, pk(ox, oy));
       if (k == 0) {
         stash[slot * 4 + 0] = pk(rax, ray); stash[slot * 4 + 1] = pk(rgx, rgy); stash[slot * 4 + 2] = pk(ax0, ay0);
       }
@@ -792,14 +800,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
     if (own >= 0) {
       const int32_t ag = stash[own * 4 + 0], go = stash[own * 4 + 1], a0 = stash[own * 4 + 2];
       ax = px(ag); ay = py(ag); gx = px(go); gy = py(go);
-      p.agent[i] = ag;
-      p.goal[i] = go;
-      const double td = calc_dist(ax, ay, gx, gy);
-      p.prev_dist[i] = a0 == ag ? td : calc_dist(gx, gy, px(a0), py(a0));   // pre-resample distance (Q9)
-      p.total_dist[i] = td;
-      p.ep_return[i] = 0.0;
-      p.ep_len[i] = 0;
-      p.episode[i] = episode + 1u;
+      esink(own, ag, go, a0);
       ncnt = 0;
 #pragma unroll
       for (int r = 0; r < K; ++r) xrows[r] = wrows[own * K + r];
@@ -1208,10 +1209,30 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     const unsigned long long m = __ballot(valid && do_reset);
     static_assert(!FIXED || (RCAP >= (BLOCK_THREADS / 64) * 16 && 16 * KR >= (64 / (NSC + NDC + !FIXED)) * (KR + 4)), "wave reset scratch");
     // one finished env (the common case): the lean single-env pass; several: up to 3 per pass
+    // a reset env's new state goes straight to HBM
+    auto osink = [&](int, int k, int il, int32_t o) {
+      if (k < NSC) {
+        (p.static_obs + (size_t)k * N)[il] = o;
+      } else {
+        (p.dyn_obs + (size_t)(k - NSC) * N)[il] = o;
+        (p.dyn_goal + (size_t)(k - NSC) * N)[il] = (uint8_t)(k - NSC);
+      }
+    };
+    auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
+      p.agent[i] = ag;
+      p.goal[i] = go;
+      const double td = reset_dists(ag, go, a0, p.prev_dist[i]);
+      p.total_dist[i] = td;
+      p.ep_return[i] = 0.0;
+      p.ep_len[i] = 0;
+      p.episode[i] = episode + 1u;
+    };
     if (m && !(m & (m - 1)))
-      wave_resets<WT, NSC, NDC, 1>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0]);
+      wave_resets<WT, NSC, NDC, 1>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0],
+                                   osink, esink);
     else if (m)
-      wave_resets<WT, NSC, NDC, 64>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0]);
+      wave_resets<WT, NSC, NDC, 64>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0],
+                                    osink, esink);
   }
   DIAG(3);
 
@@ -1436,6 +1457,222 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   }
 }
 
+// ------------------------------------------------------------------ fused multi-step rollout
+// rollout_kernel<W, NS, ND>: p.steps consecutive be_step calls of the fixed-shape kernel in one
+// launch, for a caller-given (steps, N) action tape.  Each env's state stays in registers for
+// the whole rollout; per step only the action is read and the reward / done (/ truncated,
+// final return / length) and the obs row are written, into (steps, N, ...) buffers.  State
+// goes back to HBM once, at the end.  Every draw is Philox keyed by (global env id, episode,
+// ep_len), so the outputs are bit-identical to p.steps launches of be_kernel<W, STEP, NS, ND>
+// (tests/test_gpu_parity.py::test_rollout_matches_steps); the per-step physics below is that
+// kernel's fixed-shape path (ballenv_env.py:232-289, 323-353, 200-229; ball_cnn_ac3.py:384-412).
+// Autoreset is wave-cooperative (wave_resets) with the new state stashed in LDS and picked up
+// by the env's own lane.  SURVEY 8(d) prices this mode at 1 + 8 + 1 + (4+W^2) bytes per
+// env-step plus the state round trip once per launch.
+template <int WT, int NSC, int NDC>
+__global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
+  constexpr int KR = Geo<WT>::K, F = Geo<WT>::F, G = NSC + NDC, NWAVE = BLOCK_THREADS / 64;
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Tables t;
+  __shared__ uint32_t s_rows[NWAVE][16 * KR];    // wave_resets scratch (row masks + stash)
+  __shared__ int32_t s_ost[NWAVE][64];           // a reset pass's new obstacle positions [slot][k]
+  constexpr int TW = (int)(sizeof(Tables) / 4);
+  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int blk0 = (int)blockIdx.x * BLOCK_THREADS, i = blk0 + tid, e0 = blk0 + w * 64;
+  const bool valid = i < N;
+  const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
+  NearList<BLOCK_THREADS> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
+  uint8_t* stage = smem + (size_t)(G + 1) * BLOCK_THREADS * 4 + (size_t)w * 64 * F;   // this wave's 64 rows
+
+  // ---- state into registers (straight-line, use order)
+  const uint32_t tword = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid, TW - 1));
+  uint32_t episode = ld_s(p.episode, ic);
+  int len = ld_s(p.ep_len, ic);
+  int a = ld_s(p.actions, ic);
+  const int32_t agent0 = ld_s(p.agent, ic);
+  int32_t goal = ld_s(p.goal, ic);
+  int32_t dp[NDC], so[NSC];
+  int dgi[NDC];
+#pragma unroll
+  for (int j = 0; j < NDC; ++j) { dp[j] = ld_s(p.dyn_obs + (size_t)j * N, ic); dgi[j] = ld_s(p.dyn_goal + (size_t)j * N, ic); }
+#pragma unroll
+  for (int j = 0; j < NSC; ++j) so[j] = ld_s(p.static_obs + (size_t)j * N, ic);
+  double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic), ret = ld_s(p.ep_return, ic);
+  // stats slot of this wave (be_stats_slots: one per 64 envs; a wave past N has none)
+  double* slot = (p.stats && e0 < N) ? p.stats + ((size_t)blockIdx.x * NWAVE + w) * 8 : nullptr;
+  WaveStats acc{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
+  if (slot) acc = WaveStats{slot[0], slot[1], slot[2], slot[3], slot[4], slot[5]};
+  reinterpret_cast<uint32_t*>(&t)[min(tid, TW - 1)] = tword;
+  __syncthreads();   // the only block barrier: tables staged
+
+  int ax = px(agent0), ay = py(agent0);
+  uint32_t st_flags = 0;
+  bool was_reset = false;   // statics / goal / total / episode changed: store them at the end
+  const Win g0(p, 0, 0);
+  const uint32_t R2 = (uint32_t)g0.R2;
+  const NearBox nb0(g0);
+  const int bxo = p.speed_x * (p.window / 2) + g0.R, byo = p.speed_y * (p.window / 2) + g0.R;
+  typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+  const v2s boxo = {(short)bxo, (short)byo};
+  const v2u boxw = {(unsigned short)nb0.bw, (unsigned short)nb0.bh};
+
+  for (int s = 0; s < p.steps; ++s) {
+    const size_t so_n = (size_t)s * N;
+    // next step's action: in flight while this step runs
+    const int a_next = s + 1 < p.steps ? ld_s(p.actions + so_n + N, ic) : 0;
+    const int gx = px(goal), gy = py(goal);
+    // ---- action -> agent move + clamp (ballenv_env.py:247-259)
+    st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
+    const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
+    const int dx = (int)((p.amx >> sh) & 3u) - 1, dy = (int)((p.amy >> sh) & 3u) - 1;
+    ax = min(max(ax + p.speed_x * dx, 0), p.screen_w);
+    ay = min(max(ay + p.speed_y * dy, 0), p.screen_h);
+    bool hs = false, hd = false;
+    nl.cnt = 0;
+    // ---- dynamic obstacles (counter == ep_len mod (G+1): all start at 0 on reset)
+    int counter = (int)((double)len * p.inv_g1);
+    counter = len - counter * (p.goal_change + 1);
+    if (counter < 0) counter += p.goal_change + 1;
+    if (counter > p.goal_change) counter -= p.goal_change + 1;
+    const bool change = counter >= p.goal_change;
+    const u4 b0 = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+    u4 b1{0u, 0u, 0u, 0u};
+    if (NDC > 5) b1 = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 1u), p.seed);
+    const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
+    auto obstacle_pk = [&](int32_t opk, bool& hit) {   // be_kernel's packed int16x2 test
+      const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
+      hit |= (uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2;
+      const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
+      const v2u over = __builtin_elementwise_sub_sat(b, boxw);
+      nl.base[nl.cnt * BLOCK_THREADS] = __builtin_bit_cast(uint32_t, d);
+      nl.cnt += __builtin_bit_cast(uint32_t, over) == 0u ? 1 : 0;
+    };
+#pragma unroll
+    for (int j = 0; j < NDC; ++j) {
+      int ox = px(dp[j]), oy = py(dp[j]);
+      const uint32_t wf = j < 5 ? pick_field(b0, j) : pick_field(b1, j - 5);
+      dgi[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[j], change, wf, st_flags);
+      dp[j] = pk(ox, oy);
+      obstacle_pk(dp[j], hd);
+    }
+#pragma unroll
+    for (int j = 0; j < NSC; ++j) obstacle_pk(so[j], hs);
+
+    // ---- distance, reward, done (ballenv_env.py:268-286, 200-229)
+    const double dist = calc_dist(gx, gy, ax, ay);
+    double reward = 0.0 - p.time_penalty;
+    reward += (old_dist - dist) / total;
+    if (hs) reward -= p.static_penalty;          // statics come first in obstacle_list (Q3)
+    else if (hd) reward -= p.dynamic_penalty;
+    ret += reward;
+    ++len;
+    const bool env_done = (dist < p.threshold_goal) || hs || hd;
+    const bool trunc = p.time_limit > 0 && len >= p.time_limit;
+    const bool done = env_done || trunc;
+    old_dist = dist;
+    if (valid) {
+      p.reward[so_n + i] = reward;
+      p.done[so_n + i] = (uint8_t)done;
+      if (p.truncated) p.truncated[so_n + i] = (uint8_t)(trunc && !env_done);
+      if (done) {
+        if (p.final_return) p.final_return[so_n + i] = ret;
+        if (p.final_len) p.final_len[so_n + i] = len;
+      }
+    }
+    if (slot) {   // the step kernel's per-wave fold, step by step (same order: bit-identical sums)
+      const WaveStats ws = wave_stats(done && valid, ret, len);
+      if (ws.n > 0.0) {
+        acc.n += ws.n; acc.s1 += ws.s1; acc.s2 += ws.s2; acc.sl += ws.sl;
+        acc.mn = fmin(acc.mn, ws.mn); acc.mx = fmax(acc.mx, ws.mx);
+      }
+    }
+
+    // ---- autoreset: new state stashed in LDS, picked up into this lane's registers
+    uint32_t xrows[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) xrows[k] = 0u;
+    int gxr = gx, gyr = gy;
+    const unsigned long long m = __ballot(valid && done && p.autoreset);
+    if (m) {
+      int32_t* ost = &s_ost[w][0];
+      auto osink = [&](int sl, int k, int, int32_t o) { ost[sl * G + k] = o; };
+      auto esink = [&](int own, int32_t ag, int32_t go, int32_t a0) {
+        goal = go;
+        total = reset_dists(ag, go, a0, old_dist);
+        ret = 0.0; len = 0; ++episode; was_reset = true;
+#pragma unroll
+        for (int k = 0; k < NSC; ++k) so[k] = ost[own * G + k];
+#pragma unroll
+        for (int j = 0; j < NDC; ++j) { dp[j] = ost[own * G + NSC + j]; dgi[j] = j; }
+      };
+      if (!(m & (m - 1)))
+        wave_resets<WT, NSC, NDC, 1>(p, t, m, i, gid, episode, ax, ay, gxr, gyr, nl.cnt, xrows, &s_rows[w][0], osink, esink);
+      else
+        wave_resets<WT, NSC, NDC, 64>(p, t, m, i, gid, episode, ax, ay, gxr, gyr, nl.cnt, xrows, &s_rows[w][0], osink, esink);
+    }
+
+    // ---- observation (prep_state4) into this wave's stage, then 64 rows out
+    {
+      const Win g(p, ax, ay);
+      uint32_t rows[KR], flat[Geo<WT>::NW];
+      raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, t.hw);
+#pragma unroll
+      for (int k = 0; k < KR; ++k) rows[k] |= xrows[k];
+      flatten<WT>(rows, flat);
+      const int quad = quadrant(ax, ay, gxr, gyr);
+      if constexpr ((F & 7) == 0) {   // 8-byte LDS stores
+        auto word = [&](int wd) -> uint32_t {
+          const int jc = 4 * (wd - 1);
+          return wd == 0 ? 1u << (8 * quad) : (((flat[jc >> 5] >> (jc & 31)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        };
+        uint2* dst = reinterpret_cast<uint2*>(stage + lane * F);
+#pragma unroll
+        for (int wd = 0; wd < F / 8; ++wd) dst[wd] = make_uint2(word(2 * wd), word(2 * wd + 1));
+      } else {
+        stage_row<WT>(stage, lane, flat, quad);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    copy_out<64>(stage, F, max(0, min(64, N - e0)), (int64_t)e0, p.obs + so_n * F, nullptr, lane);
+    // the next step's stage writes must follow this step's stage reads (LDS ops issue in order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    a = a_next;
+  }
+
+  // ---- state back to HBM, once
+  if (valid) {
+    p.agent[i] = pk(ax, ay);
+    p.prev_dist[i] = old_dist;
+    p.ep_return[i] = ret;
+    p.ep_len[i] = len;
+#pragma unroll
+    for (int j = 0; j < NDC; ++j) {
+      (p.dyn_obs + (size_t)j * N)[i] = dp[j];
+      (p.dyn_goal + (size_t)j * N)[i] = (uint8_t)dgi[j];
+    }
+    if (was_reset) {
+      p.goal[i] = goal;
+      p.total_dist[i] = total;
+      p.episode[i] = episode;
+#pragma unroll
+      for (int k = 0; k < NSC; ++k) (p.static_obs + (size_t)k * N)[i] = so[k];
+    }
+  }
+  if (slot && lane == 0) {
+    slot[0] = acc.n; slot[1] = acc.s1; slot[2] = acc.s2; slot[3] = acc.sl; slot[4] = acc.mn; slot[5] = acc.mx;
+  }
+  if (__ballot(st_flags != 0u)) {
+    uint32_t f = st_flags;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
+    if (lane == 0) atomicOr(p.status, (int)f);
+  }
+}
+
 __global__ void sample_actions_kernel(uint8_t* out, int32_t n, int32_t steps, int64_t env_offset,
                                       int32_t num_actions, unsigned long long seed) {
   int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1482,6 +1719,17 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false) {
   const int stage_bytes = staged ? L.epb * F : 0;
   L.lds = (near_bytes + stage_bytes + 15) & ~15;
   if (L.lds == 0) L.lds = 16;
+  return L;
+}
+
+// The fused rollout kernel for the same fixed shapes (nullptr: not applicable).
+Launch pick_rollout(const be_config& c, bool fixed_ok) {
+  Launch L{nullptr, BLOCK_THREADS, 0};
+  const bool fixed = fixed_ok && c.num_static == FIX_NS && c.num_dynamic == FIX_ND && c.speed_x == 1 &&
+                     c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
+  if (fixed && c.window == 10) L.fn = rollout_kernel<10, FIX_NS, FIX_ND>;
+  else if (fixed && c.window == 5) L.fn = rollout_kernel<5, FIX_NS, FIX_ND>;
+  L.lds = ((FIX_NS + FIX_ND + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * (4 + c.window * c.window) + 15) & ~15;
   return L;
 }
 
@@ -1784,6 +2032,45 @@ int be_step(be_ctx* ctx, const be_state* st, const uint8_t* actions, const int16
   KParams a = make_params(ctx, st, out);
   a.actions = actions; a.deltas = action_deltas; a.tape = draw_tape;
   return launch(ctx, MODE_STEP, a, stream);
+}
+
+int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t steps, const be_out* out,
+               void* stream) {
+  if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
+  if (int rc = check_state(ctx, st)) return rc;
+  if (!actions || steps < 0) return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs actions and steps >= 0");
+  if (!out || !out->obs || !out->reward || !out->done)
+    return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs out->obs, out->reward and out->done");
+  if (out->obs_f32 || out->terminal_obs)
+    return fail(ctx, BE_E_INVALID, "%s", "be_rollout writes u8 obs only (obs_f32 / terminal_obs must be NULL)");
+  const int64_t N = ctx->cfg.num_envs, F = 4 + (int64_t)ctx->cfg.window * ctx->cfg.window;
+  if (((uintptr_t)out->obs & 15) || (N * F) % 16)
+    return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs a 16-byte aligned obs and num_envs * (4+W*W) % 16 == 0");
+  if (steps == 0) return BE_OK;
+  const Launch L = pick_rollout(ctx->cfg, !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals);
+  if (L.fn) {
+    KParams a = make_params(ctx, st, out);
+    a.actions = actions; a.steps = steps;
+    int cur = -1;
+    HIP_TRY(ctx, hipGetDevice(&cur));
+    if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
+    hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
+    HIP_TRY(ctx, hipGetLastError());
+    return BE_OK;
+  }
+  // any other config: one be_step per step into the (steps, N, ...) slices (same results)
+  for (int32_t s = 0; s < steps; ++s) {
+    be_out o = *out;
+    o.obs = out->obs + s * N * F;
+    o.reward = out->reward + s * N;
+    o.done = out->done + s * N;
+    if (o.truncated) o.truncated = out->truncated + s * N;
+    if (o.final_return) o.final_return = out->final_return + s * N;
+    if (o.final_len) o.final_len = out->final_len + s * N;
+    if (int rc = be_step(ctx, st, actions + s * N, nullptr, nullptr, &o, stream)) return rc;
+  }
+  return BE_OK;
 }
 
 int be_observe(be_ctx* ctx, const be_state* st, const be_out* out, void* stream) {

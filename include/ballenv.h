@@ -172,6 +172,20 @@ int be_reset(be_ctx* ctx, const be_state* st, const uint8_t* mask,
 int be_step(be_ctx* ctx, const be_state* st, const uint8_t* actions, const int16_t* action_deltas,
             const int16_t* draw_tape, const be_out* out, void* stream);
 
+/* `steps` consecutive be_step calls in one launch (a fused rollout), for an action tape.
+ * actions: (steps, N) u8 indices into cfg.actions.  Outputs are per step: out->obs
+ * (steps, N, 4+W*W) u8, out->reward (steps, N) f64, out->done / truncated (steps, N) u8,
+ * out->final_return / final_len (steps, N) (done rows only); out->stats accumulates as for
+ * be_step.  out->obs_f32 and out->terminal_obs must be NULL; N*(4+W*W) must be a multiple of 16.
+ * Results are bit-identical to `steps` be_step calls with actions + s*N (same state, same
+ * Philox draws).  The reference has no batched counterpart: it is the caller's loop
+ *   for t: state, reward, done, _ = env.step(move_list[a_t]); prep_state4(state)
+ * (examples/ball_cnn_ac3.py:573-600 over ballenv_env.py:232-289), run for every env.
+ * The default shape (13 static + 5 dynamic obstacles, W 5 or 10, unit moves) runs one kernel
+ * that keeps each env's state in registers; other configs loop be_step.             */
+int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t steps, const be_out* out,
+               void* stream);
+
 /* prep_state4 of the current state of every env (no state change). */
 int be_observe(be_ctx* ctx, const be_state* st, const be_out* out, void* stream);
 

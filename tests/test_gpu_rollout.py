@@ -1,0 +1,95 @@
+"""be_rollout (fused multi-step) == that many be_step calls, bit for bit.
+
+The fused kernel keeps each env's state in registers for K steps; every Philox
+draw is keyed by per-env state, so its per-step outputs (obs, reward, done,
+truncated, final return/length), the state it leaves and the per-wave stats
+slots must equal K launches of the fixed-shape step kernel exactly.  Configs
+outside the fixed shape take be_rollout's be_step loop and are checked the same
+way.  The step path itself is pinned to the oracle / reference golden vectors in
+test_gpu_parity.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import KEYS, make_env, np_state
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_pair(cfg_py, N, W, K, chunks, seed=7):
+    """Env A: K be_step calls.  Env B: be_rollout over `chunks` (step counts summing to K)."""
+    a, b = make_env(cfg_py, N, W, "cuda:0", seed=seed), make_env(cfg_py, N, W, "cuda:0", seed=seed)
+    acts = a.sample_actions(K, seed=seed + 1)
+    a.reset()
+    b.reset()
+    F = 4 + W * W
+    ref = {"obs": np.empty((K, N, F), np.uint8), "reward": np.empty((K, N)), "done": np.empty((K, N), bool),
+           "truncated": np.empty((K, N), bool), "final_return": np.empty((K, N)), "final_len": np.empty((K, N), np.int32)}
+    for t in range(K):
+        obs, r, d, info = a.step(acts[t])
+        ref["obs"][t], ref["reward"][t], ref["done"][t] = obs.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy()
+        ref["truncated"][t] = info["truncated"].cpu().numpy()
+        ref["final_return"][t] = info["final_return"].cpu().numpy()
+        ref["final_len"][t] = info["final_len"].cpu().numpy()
+    t0 = 0
+    for k in chunks:
+        obs, r, d, info = b.rollout(acts[t0:t0 + k])
+        sl = slice(t0, t0 + k)
+        np.testing.assert_array_equal(obs.cpu().numpy(), ref["obs"][sl], err_msg=f"obs, steps {t0}..")
+        np.testing.assert_array_equal(r.cpu().numpy(), ref["reward"][sl], err_msg=f"reward, steps {t0}..")
+        np.testing.assert_array_equal(d.cpu().numpy(), ref["done"][sl], err_msg=f"done, steps {t0}..")
+        np.testing.assert_array_equal(info["truncated"].cpu().numpy(), ref["truncated"][sl])
+        dm = ref["done"][sl]   # final_* are written for done rows only
+        np.testing.assert_array_equal(info["final_return"].cpu().numpy()[dm], ref["final_return"][sl][dm])
+        np.testing.assert_array_equal(info["final_len"].cpu().numpy()[dm], ref["final_len"][sl][dm])
+        t0 += k
+    assert t0 == K
+    sa, sb = np_state(a), np_state(b)
+    for k in KEYS:
+        np.testing.assert_array_equal(sb[k], sa[k], err_msg=f"final state[{k}]")
+    np.testing.assert_array_equal(b.stats_buf.cpu().numpy(), a.stats_buf.cpu().numpy())
+    a.status()
+    b.status()
+    n_done = int(ref["done"].sum())
+    a.close()
+    b.close()
+    return n_done
+
+
+@pytest.mark.parametrize("W,N", [(10, 65536), (5, 4096), (10, 1008)])
+def test_rollout_matches_steps_default(gpu, W, N):
+    """Default config (fixed shape -> the fused kernel); N=1008 leaves a partial last block."""
+    from gym_ballenv_amd.config import EnvConfig
+    n_done = _run_pair(EnvConfig(), N, W, 60, (1, 25, 34))
+    assert n_done > 0
+
+
+@pytest.mark.parametrize("W", [10, 5])
+def test_rollout_mass_truncation(gpu, W):
+    """time_limit 20: every env of every wave resets on the same steps (multi-env reset passes)."""
+    from gym_ballenv_amd.config import EnvConfig
+    n_done = _run_pair(EnvConfig(time_limit=20), 20000, W, 45, (45,))
+    assert n_done >= 2 * 20000
+
+
+def test_rollout_generic_config(gpu):
+    """A config outside the fixed shape (7 static + 3 dynamic, W=7): be_rollout loops be_step."""
+    from gym_ballenv_amd.config import EnvConfig
+    _run_pair(EnvConfig(num_static=7, num_dynamic=3, time_limit=30), 2048, 7, 40, (40,))
+
+
+def test_rollout_errors(gpu):
+    from gym_ballenv_amd import BallEnvError
+    from gym_ballenv_amd.config import EnvConfig
+    env = make_env(EnvConfig(), 1001, 5, gpu)   # 1001 * 29 is not a multiple of 16
+    env.reset()
+    with pytest.raises(BallEnvError, match="% 16 == 0"):
+        env.rollout(torch.zeros(3, 1001, dtype=torch.uint8, device=gpu))
+    with pytest.raises(ValueError):
+        env.rollout(torch.zeros(3, 1000, dtype=torch.uint8, device=gpu))
+    env.close()
+    env = make_env(EnvConfig(), 1024, 10, gpu, obs_f32=True)
+    with pytest.raises(ValueError, match="u8 obs only"):
+        env.rollout(torch.zeros(3, 1024, dtype=torch.uint8, device=gpu))
+    env.close()
