@@ -156,6 +156,35 @@ def policy_leg(args, gb, dev, rank, world, stream):
     del g
     ro.close()
     env.close()
+    # the same rollout fused: be_policy_rollout, select_action + step in one kernel per chunk
+    env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
+    env.reset()
+    ro = gb.Rollout(env, pol, horizon=T, backend="fused", seed=0x5E1EC7, chunk=args.rollout_chunk)
+    ro.run()                                         # warm-up horizon
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    ro.run()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    res["fused"] = {"what": f"be_policy_rollout: select_action + be_step in one kernel, {ro.chunk} steps per launch, "
+                            "packed policy in LDS, state in registers (bit-identical trajectory)",
+                    "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
+                    "kernel_us_per_step": ev0.elapsed_time(ev1) * 1e3 / T}
+    env.status()
+    ro.close()
+    env.close()
     if args.torch_policy_steps > 0:
         Tt = args.torch_policy_steps
         env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)

@@ -26,7 +26,7 @@ EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_by
            "be_last_error",
            "be_create", "be_destroy", "be_reset", "be_step", "be_rollout", "be_observe", "be_sample_actions",
            "be_status", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
-           "be_policy_bytes", "be_observe_blocks",
+           "be_policy_rollout", "be_policy_bytes", "be_observe_blocks",
            "be_board_config_default", "be_board_create", "be_board_destroy", "be_board_last_error",
            "be_board_reset", "be_board_step", "be_board_observe", "be_board_status")
 BOARD_MAX_STATIC, BOARD_MAX_ACTIONS, BOARD_FEATURES = 32, 16, 20
@@ -129,6 +129,7 @@ def lib() -> C.CDLL:
         "be_policy_destroy": (C.c_int, [vp]),
         "be_policy_load": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
         "be_policy_act": (C.c_int, [vp, P(BeState), vp, P(BeActOut), u64, vp]),
+        "be_policy_rollout": (C.c_int, [vp, P(BeState), vp, vp, i32, P(BeOut), P(BeActOut), u64, vp]),
         "be_policy_bytes": (i64, [vp]),
         "be_observe_blocks": (C.c_int, [vp, P(BeState), vp, vp, vp]),
         "be_board_config_default": (C.c_int, [P(BeBoardConfig), i32, i32]),

@@ -26,7 +26,7 @@ ARCH = os.environ.get("BALLENV_OFFLOAD_ARCH", "gfx950")
 
 BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}"]
 UNITS = {"ballenv.hip": [], "policy.hip": ["-fno-slp-vectorize"], "features.hip": [], "board.hip": []}
-HEADERS = [HDR, os.path.join(CSRC, "philox.h"), os.path.join(CSRC, "internal.h")]
+HEADERS = [HDR, os.path.join(CSRC, "philox.h"), os.path.join(CSRC, "internal.h"), os.path.join(CSRC, "policy_core.h")]
 
 
 def _stale(out, deps):

@@ -50,6 +50,7 @@
 #include "ballenv.h"
 #include "internal.h"
 #include "philox.h"
+#include "policy_core.h"
 
 namespace {
 
@@ -101,13 +102,22 @@ struct KParams {
   uint32_t amx, amy;           // action a's (dx+1, dy+1) at bits 2a..2a+1 (every move in {-1,0,1})
   int32_t num_goals;           // goals pairwise distinct: newGoalList(g)[pick] = pick + (pick >= g)
   int32_t steps;               // rollout_kernel: steps per launch (actions / outputs are (steps, N, ...))
+  // fused policy rollouts (rollout_kernel with HT > 0, be_policy_rollout)
+  int32_t pol_bytes, pol_actions;
+  const uint8_t* pol_img;      // packed Policy(W) image (policy_core.h PolLayout)
+  const uint8_t* obs_in;       // (N, F) obs of the current state: step 0's policy input
+  uint8_t* obs_last;           // (N, F) obs after the last step, or NULL
+  uint8_t* act_out; float* logp_out; float* value_out;   // (steps, N)
+  unsigned long long pol_seed;
 };
 
 // Diagnostic phase-skip bits (timing ablations only; outputs are wrong when set).  Only
 // diagnostics builds (-DBE_DIAG_STAMPS or -DBE_DIAG_SKIP) read them; in production DBG(x) is 0.
 enum : uint32_t { DBG_NO_STATS = 1, DBG_NO_RASTER = 2, DBG_NO_OBS = 4, DBG_NO_PHILOX = 8, DBG_NO_DYN = 16,
                   DBG_NO_NEAR = 32, DBG_EXIT_ENTRY = 64, DBG_EXIT_BARRIER = 128, DBG_EXIT_PHYSICS = 256,
-                  DBG_EXIT_RASTER = 512, DBG_WAIT_LOADS = 1024 };
+                  DBG_EXIT_RASTER = 512, DBG_WAIT_LOADS = 1024,
+                  // fused policy rollout: every env on the table / no select_action tail / no block barriers
+                  DBG_POL_TABLE = 2048, DBG_POL_NO_FINISH = 4096, DBG_POL_NO_SYNC = 8192 };
 #if defined(BE_DIAG_STAMPS) || defined(BE_DIAG_SKIP)
 #define DBG(x) (p.dbg & (x))
 #else
@@ -1464,14 +1474,25 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
 // final return / length) and the obs row are written, into (steps, N, ...) buffers.  State
 // goes back to HBM once, at the end.  Every draw is Philox keyed by (global env id, episode,
 // ep_len), so the outputs are bit-identical to p.steps launches of be_kernel<W, STEP, NS, ND>
-// (tests/test_gpu_parity.py::test_rollout_matches_steps); the per-step physics below is that
-// kernel's fixed-shape path (ballenv_env.py:232-289, 323-353, 200-229; ball_cnn_ac3.py:384-412).
-// Autoreset is wave-cooperative (wave_resets) with the new state stashed in LDS and picked up
-// by the env's own lane.  SURVEY 8(d) prices this mode at 1 + 8 + 1 + (4+W^2) bytes per
-// env-step plus the state round trip once per launch.
-template <int WT, int NSC, int NDC>
+// (tests/test_gpu_rollout.py); the per-step physics below is that kernel's fixed-shape path
+// (ballenv_env.py:232-289, 323-353, 200-229; ball_cnn_ac3.py:384-412).  Autoreset is
+// wave-cooperative (wave_resets) with the new state stashed in LDS and picked up by the env's
+// own lane.  SURVEY 8(d) prices this mode at 1 + 8 + 1 + (4+W^2) bytes per env-step plus the
+// state round trip once per launch.
+//
+// HT > 0: the fused config-5 rollout (be_policy_rollout).  The action of every step comes from
+// select_action on the obs in the block's LDS stage (policy_core.h, the packed Policy(W) image
+// staged in LDS once per launch): envs with a lit window cell are compacted into a block list
+// and go through tile_forward in 16-env MFMA tiles (one wave per tile), the others take the
+// empty-window table; policy_finish draws the action.  Same functions, same inputs and the
+// same Philox keys as be_policy_act, so the trajectory is bit-identical to the two-launch
+// loop (tests/test_gpu_rollout.py::test_policy_rollout_matches_two_launch_loop).  The obs is
+// written per step only when recorded (p.obs), and the last one to p.obs_last.
+template <int WT, int NSC, int NDC, int HT = 0, int KS = 1, int NO = 10>
 __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   constexpr int KR = Geo<WT>::K, F = Geo<WT>::F, G = NSC + NDC, NWAVE = BLOCK_THREADS / 64;
+  constexpr bool POL = HT > 0;
+  constexpr PolLayout PL = pol_layout(HT > 0 ? HT : 1, KS, NO);
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Tables t;
   __shared__ uint32_t s_rows[NWAVE][16 * KR];    // wave_resets scratch (row masks + stash)
@@ -1480,15 +1501,21 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int blk0 = (int)blockIdx.x * BLOCK_THREADS, i = blk0 + tid, e0 = blk0 + w * 64;
   const bool valid = i < N;
+  const int nrows = max(0, min(64, N - e0));     // this wave's valid obs rows
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
   NearList<BLOCK_THREADS> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
-  uint8_t* stage = smem + (size_t)(G + 1) * BLOCK_THREADS * 4 + (size_t)w * 64 * F;   // this wave's 64 rows
+  uint8_t* stage_blk = smem + (size_t)(G + 1) * BLOCK_THREADS * 4;   // [256 envs][F]: row = tid
+  uint8_t* stage = stage_blk + (size_t)w * 64 * F;                    // this wave's 64 rows
+  // POL: PolLayout image + scratch, 16-byte aligned (a constant offset from the LDS base keeps the
+  // accesses ds_* -- an integer round trip of the pointer would turn them into flat accesses)
+  constexpr int POL_OFF = ((G + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * F + 15) & ~15;
+  uint8_t* pimg = smem + POL_OFF;
 
   // ---- state into registers (straight-line, use order)
   const uint32_t tword = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid, TW - 1));
   uint32_t episode = ld_s(p.episode, ic);
   int len = ld_s(p.ep_len, ic);
-  int a = ld_s(p.actions, ic);
+  int a = POL ? 0 : ld_s(p.actions, ic);
   const int32_t agent0 = ld_s(p.agent, ic);
   int32_t goal = ld_s(p.goal, ic);
   int32_t dp[NDC], so[NSC];
@@ -1503,7 +1530,31 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   WaveStats acc{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   if (slot) acc = WaveStats{slot[0], slot[1], slot[2], slot[3], slot[4], slot[5]};
   reinterpret_cast<uint32_t*>(&t)[min(tid, TW - 1)] = tword;
-  __syncthreads();   // the only block barrier: tables staged
+  int pquad = 0;          // POL: quadrant of the current obs
+  bool pnz = false;       // POL: the current obs needs the dense forward (a lit cell / not one-hot)
+  if constexpr (POL) {
+    // the packed policy image, once per launch; the current obs rows (obs of the state)
+    const uint4* src = reinterpret_cast<const uint4*>(p.pol_img);
+    for (int k = tid; k < p.pol_bytes / 16; k += BLOCK_THREADS) reinterpret_cast<uint4*>(pimg)[k] = src[k];
+    const int bytes = nrows * F;
+    const uint8_t* orow = p.obs_in + (size_t)e0 * F;
+    for (int v = lane; v < bytes / 16; v += 64) reinterpret_cast<uint4*>(stage)[v] = reinterpret_cast<const uint4*>(orow)[v];
+    for (int b = (bytes & ~15) + lane; b < bytes; b += 64) stage[b] = orow[b];
+    if (tid < 3) reinterpret_cast<int*>(pimg + PL.count)[tid] = 0;
+  }
+  __syncthreads();   // tables (and the policy image, the obs rows, the list counters) staged
+  float* pbuf_base = reinterpret_cast<float*>(pimg + PL.lds);   // POL: chunk partials of a round of tiles
+  if constexpr (POL) {
+    if (valid) {   // what be_policy_act's scan decides from the same bytes
+      const uint8_t* row = stage + lane * F;
+      const uint32_t q4 = (uint32_t)row[0] | ((uint32_t)row[1] << 8) | ((uint32_t)row[2] << 16) | ((uint32_t)row[3] << 24);
+      uint32_t lit = 0;
+      for (int b = 4; b < F; ++b) lit |= row[b];
+      pquad = q4 == 1u ? 0 : (q4 == 0x100u ? 1 : (q4 == 0x10000u ? 2 : 3));
+      const bool onehot = q4 == 1u || q4 == 0x100u || q4 == 0x10000u || q4 == 0x1000000u;
+      pnz = lit != 0u || !onehot;
+    }
+  }
 
   int ax = px(agent0), ay = py(agent0);
   uint32_t st_flags = 0;
@@ -1518,8 +1569,116 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
 
   for (int s = 0; s < p.steps; ++s) {
     const size_t so_n = (size_t)s * N;
-    // next step's action: in flight while this step runs
-    const int a_next = s + 1 < p.steps ? ld_s(p.actions + so_n + N, ic) : 0;
+    // next step's action (tape mode): in flight while this step runs
+    const int a_next = (!POL && s + 1 < p.steps) ? ld_s(p.actions + so_n + N, ic) : 0;
+    if constexpr (POL) {
+      // ---- select_action (ball_cnn_ac3.py:210-220) on the obs in the stage
+      // list counters, one per step mod 3: thread 0 clears step s+2's right after this step's
+      // barrier, which every wave passes again (step s+1) before it counts into that one
+      int* cnt3 = reinterpret_cast<int*>(pimg + PL.count);
+      int16_t* list = reinterpret_cast<int16_t*>(pimg + PL.list);
+      float* lg = reinterpret_cast<float*>(pimg + PL.logits);
+      if (DBG(DBG_POL_TABLE)) pnz = false;
+      const int c3 = s % 3;
+      // the draw's uniform, a function of this env's state (in flight across the barrier)
+      const float u = policy_uniform(gid, episode, (uint32_t)len, p.pol_seed);
+      if (valid && pnz) list[atomicAdd(&cnt3[c3], 1)] = (int16_t)tid;
+      if (!DBG(DBG_POL_NO_SYNC)) __syncthreads();   // list complete (and every wave's stage rows written)
+      const int cnt = cnt3[c3];
+      if (tid == 0) cnt3[c3 == 0 ? 2 : c3 - 1] = 0;   // (s + 2) % 3
+      const int g4 = lane >> 4;
+      // the listed envs in 16-env tiles, rounds of up to NWAVE tiles: every wave runs its chunk
+      // of hidden rows (tile_chunk, wave w = chunk w) for each tile of the round into pbuf, then
+      // the listed envs' lanes add the four chunks in order (tile_forward's sum, bit for bit)
+      float* pbuf = pbuf_base;   // [NWAVE chunks][NWAVE tiles][16][NO]
+      const int ntiles = (cnt + 15) >> 4;
+      for (int r0 = 0; r0 < ntiles; r0 += NWAVE) {
+        const int nt = min(NWAVE, ntiles - r0);
+        // obs fragments of tile r0 + tt (load_obs16's bytes: row e, columns c .. c+15, zero past F)
+        auto load_b = [&](int tt, v4i (&Bt)[KS]) {
+          const int k = (r0 + tt) * 16 + (lane & 15);
+          const int e = k < cnt ? list[k] : -1;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const int c = 64 * ks + 16 * g4;
+            const uint8_t* row = stage_blk + (e >= 0 ? e : 0) * F;
+            v4i v = {0, 0, 0, 0};
+            if constexpr ((F & 7) == 0) {
+              const int c0 = c < F - 8 ? c : F - 8, c1 = c + 8 < F - 8 ? c + 8 : F - 8;
+              const uint2 lo = *reinterpret_cast<const uint2*>(row + c0), hi = *reinterpret_cast<const uint2*>(row + c1);
+              const bool vlo = e >= 0 && c + 8 <= F, vhi = e >= 0 && c + 16 <= F;
+              v[0] = vlo ? (int)lo.x : 0; v[1] = vlo ? (int)lo.y : 0;
+              v[2] = vhi ? (int)hi.x : 0; v[3] = vhi ? (int)hi.y : 0;
+            } else {
+              uint32_t wd[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+              for (int j = 0; j < 16; ++j)
+                if (e >= 0 && c + j < F) wd[j >> 2] |= (uint32_t)row[c + j] << (8 * (j & 3));
+              v[0] = (int)wd[0]; v[1] = (int)wd[1]; v[2] = (int)wd[2]; v[3] = (int)wd[3];
+            }
+            Bt[ks] = v;
+          }
+        };
+        auto put = [&](int tt, const float (&part)[NO]) {
+          if (g4 == 0) {
+#pragma unroll
+            for (int o = 0; o < NO; ++o) pbuf[((w * NWAVE + tt) * 16 + lane) * NO + o] = part[o];
+          }
+        };
+        constexpr int HTC = HT > 0 ? HT : 1;
+        const int h0 = pol_chunk_begin(HTC, w), h1 = pol_chunk_begin(HTC, w + 1);
+        for (int tt = 0; tt < nt; tt += 2) {   // two tiles at a time: shared weight reads, interleaved chains
+          v4i Ba[KS], Bb[KS];
+          float pa[NO], pb[NO];
+          load_b(tt, Ba);
+          if (tt + 1 < nt && !DBG(0xF0000u)) {
+            load_b(tt + 1, Bb);
+            tile_chunk2<HTC, KS, NO>(pimg, Ba, Bb, lane, h0, h1, pa, pb);
+            put(tt, pa);
+            put(tt + 1, pb);
+          } else {
+            // (diagnostics builds: tile_chunk's own ablation bits 2 / 4 from dbg bits 17 / 18)
+            tile_chunk<HTC, KS, NO>(pimg, Ba, lane, (int)(DBG(0xF0000u) >> 16), h0, h1, pa);
+            put(tt, pa);
+            if (tt + 1 < nt) {
+              load_b(tt + 1, Bb);
+              tile_chunk<HTC, KS, NO>(pimg, Bb, lane, (int)(DBG(0xF0000u) >> 16), h0, h1, pb);
+              put(tt + 1, pb);
+            }
+          }
+        }
+        __syncthreads();   // every chunk of the round's tiles
+        if (tid < nt * 16 && r0 * 16 + tid < cnt) {   // one thread per listed env: the chunks in order
+          const int e = list[r0 * 16 + tid];
+          const int tt = tid >> 4, col = tid & 15;
+#pragma unroll
+          for (int o = 0; o < NO; ++o) {
+            float v = pbuf[((0 * NWAVE + tt) * 16 + col) * NO + o];
+#pragma unroll
+            for (int c = 1; c < NWAVE; ++c) v = v + pbuf[((c * NWAVE + tt) * 16 + col) * NO + o];
+            lg[e * NO + o] = v;
+          }
+        }
+        __syncthreads();   // round done: pbuf free, these logits visible
+      }
+      static_assert(NWAVE == POL_CHUNKS, "one hidden-row chunk per wave");
+      // select_action's tail (policy_finish with the uniform drawn above)
+      const float* src = pnz ? lg + tid * NO : reinterpret_cast<const float*>(pimg + PL.table) + pquad * NO;
+      float lp = 0.f, val = 0.f;
+      if (DBG(DBG_POL_NO_FINISH)) {
+        a = (int)((gid + (uint32_t)len * 7u) % 9u);
+      } else {
+        const PolDist<NO> d = policy_dist<NO>(src, reinterpret_cast<const float*>(pimg + PL.hbias), p.pol_actions,
+                                              nullptr);
+        a = policy_pick<NO>(d.cdf, d.lp, d.last_nz, p.pol_actions, u, lp);
+        val = d.value;
+      }
+      if (valid) {
+        p.act_out[so_n + i] = (uint8_t)a;
+        if (p.logp_out) p.logp_out[so_n + i] = lp;
+        if (p.value_out) p.value_out[so_n + i] = val;
+      }
+    }
     const int gx = px(goal), gy = py(goal);
     // ---- action -> agent move + clamp (ballenv_env.py:247-259)
     st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
@@ -1620,6 +1779,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       for (int k = 0; k < KR; ++k) rows[k] |= xrows[k];
       flatten<WT>(rows, flat);
       const int quad = quadrant(ax, ay, gxr, gyr);
+      if constexpr (POL) {
+        uint32_t any = 0u;
+#pragma unroll
+        for (int k = 0; k < Geo<WT>::NW; ++k) any |= flat[k];
+        pquad = quad;
+        pnz = valid && any != 0u;   // (lanes past N are never listed)
+      }
       if constexpr ((F & 7) == 0) {   // 8-byte LDS stores
         auto word = [&](int wd) -> uint32_t {
           const int jc = 4 * (wd - 1);
@@ -1632,14 +1798,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
         stage_row<WT>(stage, lane, flat, quad);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    copy_out<64>(stage, F, max(0, min(64, N - e0)), (int64_t)e0, p.obs + so_n * F, nullptr, lane);
-    // the next step's stage writes must follow this step's stage reads (LDS ops issue in order)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (p.obs) {   // recorded obs (always in tape mode)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      copy_out<64>(stage, F, nrows, (int64_t)e0, p.obs + so_n * F, nullptr, lane);
+      // the next step's stage writes must follow this step's stage reads (LDS ops issue in order)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     a = a_next;
   }
 
@@ -1661,6 +1829,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
 #pragma unroll
       for (int k = 0; k < NSC; ++k) (p.static_obs + (size_t)k * N)[i] = so[k];
     }
+  }
+  if (p.obs_last) {   // the obs of the final state (the env's obs buffer)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    copy_out<64>(stage, F, nrows, (int64_t)e0, p.obs_last, nullptr, lane);
   }
   if (slot && lane == 0) {
     slot[0] = acc.n; slot[1] = acc.s1; slot[2] = acc.s2; slot[3] = acc.sl; slot[4] = acc.mn; slot[5] = acc.mx;
@@ -1730,6 +1904,23 @@ Launch pick_rollout(const be_config& c, bool fixed_ok) {
   if (fixed && c.window == 10) L.fn = rollout_kernel<10, FIX_NS, FIX_ND>;
   else if (fixed && c.window == 5) L.fn = rollout_kernel<5, FIX_NS, FIX_ND>;
   L.lds = ((FIX_NS + FIX_ND + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * (4 + c.window * c.window) + 15) & ~15;
+  return L;
+}
+
+// The fused policy rollout kernel: fixed env shape and the select_action kernel's Policy(W)
+// shapes (H 208 / W 10 and H 128 / W 5, 9 actions).
+Launch pick_policy_rollout(const be_config& c, bool fixed_ok, int HT, int KS, int NO) {
+  Launch L{nullptr, BLOCK_THREADS, 0};
+  const bool fixed = fixed_ok && c.num_static == FIX_NS && c.num_dynamic == FIX_ND && c.speed_x == 1 &&
+                     c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
+  if (fixed && c.window == 10 && HT == 13 && KS == 2 && NO == 10)
+    L.fn = rollout_kernel<10, FIX_NS, FIX_ND, 13, 2, 10>;
+  else if (fixed && c.window == 5 && HT == 8 && KS == 1 && NO == 10)
+    L.fn = rollout_kernel<5, FIX_NS, FIX_ND, 8, 1, 10>;
+  const PolLayout PL = pol_layout(HT, KS, NO);
+  L.lds = (FIX_NS + FIX_ND + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * (4 + c.window * c.window);
+  L.lds = ((L.lds + 15) & ~15) + PL.lds;
+  L.lds = ((L.lds + 15) & ~15) + POL_CHUNKS * (BLOCK_THREADS / 64) * 16 * NO * 4;   // chunk partials
   return L;
 }
 
@@ -2072,6 +2263,29 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
   }
   return BE_OK;
 }
+
+}  // extern "C"
+
+int be_internal_policy_rollout(be_ctx* ctx, const be_state* st, const be_pol_rollout_args* r, void* stream) {
+  const Launch L = pick_policy_rollout(ctx->cfg, !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals, r->HT,
+                                       r->KS, r->NO);
+  if (!L.fn) return 0;
+  KParams a = make_params(ctx, st, r->out);
+  a.steps = r->steps;
+  a.pol_bytes = r->img_bytes; a.pol_actions = r->num_actions; a.pol_img = r->img; a.pol_seed = r->seed;
+  a.obs_in = r->obs_in; a.obs_last = r->obs_last;
+  a.act_out = r->act->action; a.logp_out = r->act->log_prob; a.value_out = r->act->value;
+  int cur = -1;
+  HIP_TRY(ctx, hipGetDevice(&cur));
+  if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int N = ctx->cfg.num_envs;
+  const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
+  hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
+  HIP_TRY(ctx, hipGetLastError());
+  return 1;
+}
+
+extern "C" {
 
 int be_observe(be_ctx* ctx, const be_state* st, const be_out* out, void* stream) {
   if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");

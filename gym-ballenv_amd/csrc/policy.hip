@@ -48,38 +48,9 @@
 #include "ballenv.h"
 #include "internal.h"
 #include "philox.h"
+#include "policy_core.h"
 
 namespace {
-
-constexpr uint32_t PURPOSE_POLICY = 5;
-constexpr int POL_MAXH = 256, POL_MAXF = 128, POL_MAXA = 15;
-constexpr int POL_ENVS = 256;                    // envs per workgroup
-constexpr int POL_THREADS = 64 * POL_ENVS / 16;  // one wave per 16-env tile
-constexpr int POL_FIN_WAVES = POL_ENVS / 64;     // waves that run the epilogue
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-
-// Packed-weight image (bytes), identical in HBM and in each workgroup's LDS.
-struct PolLayout {
-  int HT, KS, NO;            // 16-row hidden tiles, 64-wide K steps, outputs (actions + value)
-  int frag, bias, head, hbias, table, total, logits, info, list, count, lds;
-};
-__host__ __device__ constexpr PolLayout pol_layout(int HT, int KS, int NO) {
-  PolLayout L{};
-  L.HT = HT; L.KS = KS; L.NO = NO;
-  L.frag = 0;                                   // [HT][3 digits, high first][KS][64 lanes][16 B] int8
-  L.bias = L.frag + HT * 3 * KS * 1024;         // [HT*16] i32   bq_k = rint(b1_k / s_k)
-  L.head = L.bias + HT * 16 * 4;                // [HT][4 groups][NO][4] f32  W_o,k * s_k, k = 16ht+4g+r
-  L.hbias = L.head + HT * 4 * NO * 4 * 4;       // [NO] f32 (pad actions: -inf; value last)
-  L.table = L.hbias + NO * 4;                   // [4][NO] f32 raw logits of the obs e_0..e_3 (empty window)
-  L.total = (L.table + 4 * NO * 4 + 15) & ~15;
-  L.logits = L.total;                           // LDS only: [POL_ENVS][NO] f32 for the epilogue
-  L.info = L.logits + POL_ENVS * NO * 4;        // LDS only: [POL_ENVS] u8
-  L.list = L.info + POL_ENVS;                   // LDS only: [POL_ENVS] i16 envs with a lit window cell
-  L.count = L.list + POL_ENVS * 2;              // LDS only: i32
-  L.lds = L.count + 16;
-  return L;
-}
 
 struct PolPack {             // pack kernel arguments (device f32 weights in torch state_dict layout)
   const float* w1; const float* b1; const float* wa; const float* ba; const float* wv; const float* bv;
@@ -171,74 +142,6 @@ __device__ __forceinline__ v4i load_obs16(const PParams& p, int env, int c) {
   return v;
 }
 
-// x summed over lanes l, l^16, l^32, l^48 (the 4 lane groups), on the VALU
-__device__ __forceinline__ float sum_groups(float x) {
-  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
-
-#ifndef BE_POL_UNROLL
-#define BE_POL_UNROLL 13
-#endif
-
-// OR of x over lanes l, l^16, l^32, l^48
-__device__ __forceinline__ uint32_t or_groups(uint32_t x) {
-  const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-  x = a[0] | a[1];
-  const auto b = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-  return b[0] | b[1];
-}
-
-// The dense forward of one 16-env column tile (env of lane = lane & 15, obs fragments B):
-// fc1 on the int8 MFMA, relu, heads.  Returns the raw logits (before the head bias),
-// summed over the lane groups (every lane of a column holds its env's values).
-template <int HT, int KS, int NO>
-__device__ __forceinline__ void tile_forward(const uint8_t* lds, const v4i (&B)[KS], int lane, int dbg,
-                                             float (&out)[NO]) {
-  constexpr PolLayout L = pol_layout(HT, KS, NO);
-  const int g = lane >> 4;
-  float part[NO];
-#pragma unroll
-  for (int o = 0; o < NO; ++o) part[o] = 0.f;
-#pragma unroll BE_POL_UNROLL
-  for (int ht = 0; ht < HT; ++ht) {
-    v4i acc[3];   // one accumulator per digit plane: no VALU between a tile row's MFMAs
-    acc[0] = v4i{0, 0, 0, 0};
-    acc[1] = v4i{0, 0, 0, 0};
-    acc[2] = *(const v4i*)(lds + L.bias + (ht * 16 + 4 * g) * 4);
-    if (!(dbg & 2)) {
-#pragma unroll
-      for (int d = 0; d < 3; ++d)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const v4i a = *(const v4i*)(lds + L.frag + ((((ht * 3 + d) * KS + ks) * 64 + lane) << 4));
-          acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, B[ks], acc[d], 0, 0, 0);
-        }
-    } else {
-      acc[2] += B[0];
-    }
-    float h[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = (int)(((uint32_t)acc[0][r] << 16) + ((uint32_t)acc[1][r] << 8)) + acc[2][r];
-      h[r] = (float)(q > 0 ? q : 0);
-    }
-    if (!(dbg & 4)) {
-#pragma unroll
-      for (int o = 0; o < NO; ++o) {
-        const float4 w = *(const float4*)(lds + L.head + (((ht * 4 + g) * NO + o) * 4) * 4);
-        part[o] = fmaf(w.w, h[3], fmaf(w.z, h[2], fmaf(w.y, h[1], fmaf(w.x, h[0], part[o]))));
-      }
-    } else {
-      part[0] += h[0] + h[1] + h[2] + h[3];
-    }
-  }
-#pragma unroll
-  for (int o = 0; o < NO; ++o) out[o] = sum_groups(part[o]);
-}
-
 // Sparse structure of the input: an env whose window has no lit cell has the obs e_q (its
 // quadrant one-hot) -- over 90 % of envs in rollouts (0.7 % of obs have a lit cell under
 // random actions, 7.6 % under the reference's trained Policy(10)).  Their logits are the
@@ -320,38 +223,12 @@ __global__ __launch_bounds__(POL_THREADS) void policy_kernel(PParams p) {
     for (int o = 0; o < NO; ++o) p.table_out[(int64_t)my_env * NO + o] = src[o];
     return;
   }
-  const float* hb = (const float*)(lds + L.hbias);
-  float logit[NO];
-#pragma unroll
-  for (int o = 0; o < NO; ++o) logit[o] = src[o] + hb[o];
-
-  // softmax over the action logits (pads are -inf), Categorical draw by inverse CDF
-  float mx = logit[0];
-#pragma unroll
-  for (int o = 1; o < NO - 1; ++o) mx = fmaxf(mx, logit[o]);
-  float e[NO - 1], sum = 0.f;
-#pragma unroll
-  for (int o = 0; o < NO - 1; ++o) { e[o] = __expf(logit[o] - mx); sum += e[o]; }
-  const float inv = __builtin_amdgcn_rcpf(sum);
-  const u4 r = philox((uint32_t)(p.gid0 + my_env), episode, (uint32_t)len, tag(PURPOSE_POLICY, 0), p.seed);
-  const float u = (float)(r.x >> 8) * (1.0f / 16777216.0f);
-  float c = 0.f;
-  int act = 0, last_nz = 0;
-#pragma unroll
-  for (int o = 0; o < NO - 1; ++o) {
-    const float pr = e[o] * inv;
-    c += pr;
-    act += (o < p.A && c <= u) ? 1 : 0;
-    last_nz = (o < p.A && pr > 0.f) ? o : last_nz;
-    if (p.probs && o < p.A) p.probs[(int64_t)my_env * p.A + o] = pr;
-  }
-  act = act > last_nz ? last_nz : act;
-  float la = logit[0];
-#pragma unroll
-  for (int o = 1; o < NO - 1; ++o) la = o == act ? logit[o] : la;
+  float lp, val;
+  const int act = policy_finish<NO>(src, (const float*)(lds + L.hbias), p.A, (uint32_t)(p.gid0 + my_env), episode,
+                                    (uint32_t)len, p.seed, p.probs ? p.probs + (int64_t)my_env * p.A : nullptr, lp, val);
   p.action[my_env] = (uint8_t)act;
-  if (p.log_prob) p.log_prob[my_env] = (la - mx) - __logf(sum);
-  if (p.value) p.value[my_env] = logit[NO - 1];
+  if (p.log_prob) p.log_prob[my_env] = lp;
+  if (p.value) p.value[my_env] = val;
 }
 
 using PolFn = void (*)(PParams);
@@ -494,6 +371,48 @@ int be_policy_act(be_policy* pol, const be_state* st, const uint8_t* obs, const 
   const dim3 grid((unsigned)((p.n + POL_ENVS - 1) / POL_ENVS));
   hipLaunchKernelGGL(pol->k.fn, grid, dim3(POL_THREADS), (size_t)pol->L.lds, (hipStream_t)stream, p);
   POL_TRY(ctx, hipGetLastError());
+  return BE_OK;
+}
+
+int be_policy_rollout(be_policy* pol, const be_state* st, const uint8_t* obs_in, uint8_t* obs_last, int32_t steps,
+                      const be_out* out, const be_act_out* act, uint64_t seed, void* stream) {
+  if (!pol) return be_ctx_fail(nullptr, BE_E_INVALID, "policy is NULL");
+  be_ctx* ctx = pol->ctx;
+  if (!pol->loaded) return be_ctx_fail(ctx, BE_E_INVALID, "be_policy_rollout before be_policy_load");
+  if (int rc = be_ctx_check_state(ctx, st)) return rc;
+  if (!obs_in || steps < 0 || !out || !out->reward || !out->done || !act || !act->action)
+    return be_ctx_fail(ctx, BE_E_INVALID, "be_policy_rollout needs obs_in, steps >= 0, out->reward/done, act->action");
+  if (!out->obs && !obs_last) return be_ctx_fail(ctx, BE_E_INVALID, "be_policy_rollout needs out->obs or obs_last");
+  if (out->obs_f32 || out->terminal_obs || act->probs)
+    return be_ctx_fail(ctx, BE_E_INVALID, "be_policy_rollout: obs_f32, terminal_obs and probs must be NULL");
+  const int64_t N = pol->cv.num_envs, F = pol->F;
+  if (((uintptr_t)obs_in & 15) || ((uintptr_t)obs_last & 15) || ((uintptr_t)out->obs & 15) || (N * F) % 16)
+    return be_ctx_fail(ctx, BE_E_INVALID,
+                       "be_policy_rollout needs 16-byte aligned obs buffers and num_envs * (4+W*W) % 16 == 0");
+  if (steps == 0) return BE_OK;
+  if (int rc = pol_set_device(ctx, pol->cv.device)) return rc;
+  const be_pol_rollout_args r{pol->img, pol->L.total, pol->k.HT, pol->k.KS, pol->k.NO, pol->A,
+                              (unsigned long long)seed, obs_in, obs_last, steps, out, act};
+  const int rc = be_internal_policy_rollout(ctx, st, &r, stream);
+  if (rc != 0) return rc < 0 ? rc : BE_OK;
+  // no fused kernel for this shape: be_policy_act + be_step per step (the same trajectory)
+  for (int32_t s = 0; s < steps; ++s) {
+    const uint8_t* o_in = s == 0 ? obs_in : (out->obs ? out->obs + (s - 1) * N * F : obs_last);
+    const be_act_out ao{act->action + s * N, act->log_prob ? act->log_prob + s * N : nullptr,
+                        act->value ? act->value + s * N : nullptr, nullptr};
+    if (int e = be_policy_act(pol, st, o_in, &ao, seed, stream)) return e;
+    be_out o = *out;
+    o.obs = out->obs ? out->obs + s * N * F : obs_last;
+    o.reward = out->reward + s * N;
+    o.done = out->done + s * N;
+    if (o.truncated) o.truncated = out->truncated + s * N;
+    if (o.final_return) o.final_return = out->final_return + s * N;
+    if (o.final_len) o.final_len = out->final_len + s * N;
+    if (int e = be_step(ctx, st, ao.action, nullptr, nullptr, &o, stream)) return e;
+  }
+  if (out->obs && obs_last)
+    POL_TRY(ctx, hipMemcpyAsync(obs_last, out->obs + (steps - 1) * N * F, (size_t)(N * F), hipMemcpyDeviceToDevice,
+                                (hipStream_t)stream));
   return BE_OK;
 }
 

@@ -14,6 +14,10 @@ and each launch writes straight into row t of the (T, N) trajectory buffers
 kernels).  ``capture()`` records the T-step loop into HIP graphs, so
 ``run()`` is one graph replay per chunk with no host work per step.
 
+``backend="fused"`` runs the same T steps as ``be_policy_rollout`` launches of ``chunk``
+steps each: select_action and the env step in one kernel, each env's state in
+registers and the packed policy in LDS (bit-identical to ``"hip"``).
+
 ``backend="torch"`` runs select_action as plain PyTorch fp32 (``Policy`` +
 ``torch_select_action`` on ``torch.rand`` uniforms) -- the PyTorch-ROCm policy
 the BASELINE config names, kept as the comparison point.
@@ -37,9 +41,9 @@ from .policy import HipPolicy, Policy, torch_select_action
 
 class Rollout:
     def __init__(self, env, policy: Policy, horizon: int, backend: str = "hip", record_obs: bool = False,
-                 seed: int = 0x5E1EC7):
-        if backend not in ("hip", "torch"):
-            raise ValueError("backend must be 'hip' or 'torch'")
+                 seed: int = 0x5E1EC7, chunk: int = 100):
+        if backend not in ("hip", "fused", "torch"):
+            raise ValueError("backend must be 'hip', 'fused' or 'torch'")
         self.env, self.policy, self.T, self.backend = env, policy, int(horizon), backend
         dev, N, T = env.device, env.num_envs, self.T
         self.seed = int(seed)
@@ -51,7 +55,8 @@ class Rollout:
         self.obs = torch.zeros(T + 1, N, env.obs_dim, dtype=torch.uint8, device=dev) if record_obs else None
         self._graphs = []
         self._lib = _abi.lib()
-        if backend == "hip":
+        self.chunk = max(1, int(chunk))
+        if backend in ("hip", "fused"):
             self.hp = HipPolicy(env, policy, seed=self.seed)
             self._act_outs = [_abi.BeActOut(self.actions[t].data_ptr(), self.log_probs[t].data_ptr(),
                                             self.values[t].data_ptr(), None) for t in range(T)]
@@ -65,6 +70,23 @@ class Rollout:
             self._step_outs.append(_abi.BeOut(obs_ptr, o.obs_f32, self.rewards[t].data_ptr(),
                                               self.dones[t].data_ptr(), o.truncated, o.terminal_obs,
                                               o.final_return, o.final_len, o.stats))
+
+    def run_fused(self, stream_ptr=None) -> None:
+        """The horizon as be_policy_rollout launches of ``chunk`` steps (backend="fused")."""
+        env, lib, N, F = self.env, self._lib, self.env.num_envs, self.env.obs_dim
+        s = env._stream() if stream_ptr is None else stream_ptr
+        self.begin()
+        for c0 in range(0, self.T, self.chunk):
+            k = min(self.chunk, self.T - c0)
+            rec = self.obs[c0 + 1].data_ptr() if self.obs is not None else None
+            out = _abi.BeOut(rec, None, self.rewards[c0].data_ptr(), self.dones[c0].data_ptr(), None, None,
+                             None, None, env._out.stats)
+            act = _abi.BeActOut(self.actions[c0].data_ptr(), self.log_probs[c0].data_ptr(),
+                                self.values[c0].data_ptr(), None)
+            rc = lib.be_policy_rollout(self.hp._h, C.byref(env._st), env.obs.data_ptr(), env.obs.data_ptr(), k,
+                                       C.byref(out), C.byref(act), self.seed & (2**64 - 1), s)
+            if rc:
+                _abi.check(rc, env._ctx)
 
     def _obs_t(self, t: int) -> torch.Tensor:
         return self.obs[t] if self.obs is not None else self.env.obs
@@ -96,14 +118,25 @@ class Rollout:
         if self.obs is not None:
             self.obs[0].copy_(self.env.obs)
 
+    def end(self) -> None:
+        """With record_obs the steps write obs into the record: leave the last one in env.obs."""
+        if self.obs is not None:
+            self.env.obs.copy_(self.obs[self.T])
+
     def run_eager(self) -> None:
+        if self.backend == "fused":
+            return self.run_fused()
         self.begin()
         for t in range(self.T):
             self.step(t)
+        self.end()
 
     def capture(self, chunk: int = 250) -> None:
         """Record the T steps into HIP graphs of ``chunk`` steps each."""
         dev = self.env.device
+        if self.backend == "fused":     # a few launches per horizon: nothing to capture
+            self._graphs = []
+            return
         if self.backend == "torch":
             # initialise the BLAS handles eagerly: hipBLASLt set-up is not capturable
             with torch.no_grad():
@@ -122,11 +155,14 @@ class Rollout:
 
     def run(self) -> None:
         """Replay the captured horizon (capture() first)."""
+        if self.backend == "fused":
+            return self.run_fused()
         if not self._graphs:
             raise RuntimeError("capture() first")
         self.begin()
         for g in self._graphs:
             g.replay()
+        self.end()
 
     def discounted_returns(self, gamma: float = 0.99, bootstrap: Optional[torch.Tensor] = None) -> torch.Tensor:
         """R_t = r_t + gamma * R_{t+1} * (1 - done_t), per env (finish_episode, ball_cnn_ac3.py:224-227)."""

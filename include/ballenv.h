@@ -226,6 +226,18 @@ int be_policy_load(be_policy* pol, const float* fc1_w, const float* fc1_b, const
 /* Policy forward + draw for every env from obs (N, 4+W*W) u8; st supplies episode/ep_len (Philox key). */
 int be_policy_act(be_policy* pol, const be_state* st, const uint8_t* obs, const be_act_out* out, uint64_t seed,
                   void* stream);
+
+/* `steps` config-5 steps in one launch: for s in 0..steps-1
+ *   act[s] = select_action(obs_s) (as be_policy_act, same Philox draw);  be_step(act[s]) -> obs_{s+1}
+ * obs_in: (N, F) obs of the current state (obs_0, e.g. the env's obs buffer).  out: per-step
+ * (steps, N, ...) outputs as for be_rollout; out->obs (steps, N, F) records obs_1..obs_steps or is
+ * NULL; obs_last (N, F) receives obs_steps (may equal obs_in) or is NULL; one of the two is
+ * required.  act: (steps, N) action / log_prob / value (probs must be NULL).  N*F % 16 == 0.
+ * Bit-identical to the be_policy_act + be_step loop (ball_cnn_ac3.py:573-600 for every env).
+ * The default env shape with the Policy(10) / Policy(5) shapes runs one kernel with the packed
+ * weights in LDS and each env's state in registers; other shapes run that loop.          */
+int be_policy_rollout(be_policy* pol, const be_state* st, const uint8_t* obs_in, uint8_t* obs_last, int32_t steps,
+                      const be_out* out, const be_act_out* act, uint64_t seed, void* stream);
 /* Bytes of the packed weight image (staged once per workgroup in LDS). */
 int64_t be_policy_bytes(const be_policy* pol);
 
