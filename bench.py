@@ -113,6 +113,10 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
 def policy_leg(args, gb, dev, rank, world, stream):
     """BASELINE config 5: the same env batch driven by the reference's Policy(W) on the GPU.
 
+    Reported: the fused rollout (be_policy_rollout, one kernel per chunk of steps) with the
+    two-launch loop below and the PyTorch-ROCm policy as comparison points (same trajectory
+    for the two HIP paths, tests/test_gpu_rollout.py).
+
     One step = be_policy_act (select_action, csrc/policy.hip) + be_step, both
     writing into (T, N) trajectory rows, captured in HIP graphs.  The policy is
     the reference's trained Policy(W) (tests/golden/policy_w{W}.npz) when the
@@ -125,7 +129,7 @@ def policy_leg(args, gb, dev, rank, world, stream):
     torch.manual_seed(0)
     pol = Policy.from_npz(path, W) if path else Policy(W)
     res = {"workload": f"config 5: Policy({W}) select_action (be_policy_act, int8-MFMA fc1) + be_step, "
-                       f"{N} envs/GPU, T={T} steps per rollout, hipGraph replay",
+                       f"{N} envs/GPU, T={T} steps per rollout, hipGraph replay (two launches per step)",
            "weights": os.path.relpath(path, ROOT) if path else "random init"}
     env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
     env.reset()
@@ -178,10 +182,13 @@ def policy_leg(args, gb, dev, rank, world, stream):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    res["fused"] = {"what": f"be_policy_rollout: select_action + be_step in one kernel, {ro.chunk} steps per launch, "
-                            "packed policy in LDS, state in registers (bit-identical trajectory)",
-                    "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
-                    "kernel_us_per_step": ev0.elapsed_time(ev1) * 1e3 / T}
+    fused = {"workload": f"config 5: Policy({W}) select_action + be_step of {N} envs/GPU in one kernel "
+                         f"(be_policy_rollout, {ro.chunk} steps per launch, packed policy in LDS, state in "
+                         f"registers), T={T} steps; trajectory bit-identical to the two-launch loop",
+             "weights": res["weights"], "value": T * N * world / el, "unit": "env-steps/s",
+             "ms_per_step": el / T * 1e3, "kernel_us_per_step": ev0.elapsed_time(ev1) * 1e3 / T}
+    episodes = env.episode_stats()
+    fused["episodes"] = {k: episodes[k] for k in ("episodes", "mean_return", "mean_length")}
     env.status()
     ro.close()
     env.close()
@@ -194,12 +201,13 @@ def policy_leg(args, gb, dev, rank, world, stream):
         ro.capture(chunk=Tt)
         ro.run()
         el_t, _ = timed_graph_steps(ro._graphs, Tt, dev, stream, world)
-        res["torch_policy"] = {"value": Tt * N * world / el_t, "unit": "env-steps/s", "ms_per_step": el_t / Tt * 1e3,
-                               "what": "same loop with select_action in PyTorch-ROCm fp32 (Linear/softmax/cumsum "
-                                       "draw), hipGraph replay"}
+        fused["torch_policy"] = {"value": Tt * N * world / el_t, "unit": "env-steps/s", "ms_per_step": el_t / Tt * 1e3,
+                                 "what": "same loop with select_action in PyTorch-ROCm fp32 (Linear/softmax/cumsum "
+                                         "draw), hipGraph replay"}
         ro.close()
         env.close()
-    return res
+    fused["two_launch"] = res
+    return fused
 
 
 def rollout_leg(args, gb, dev, rank, world, stream):

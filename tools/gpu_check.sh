@@ -22,12 +22,14 @@ fi
 step bench 400 python bench.py ${BENCH_ARGS:-}
 tail -1 gpurun_out/bench.log
 if [ "${PROFILE:-1}" = "1" ]; then
-  # headline step kernel alone (no config-5 leg), then the config-5 policy rollout alone
+  # headline step kernel alone (no other leg), then the config-5 policy rollouts (two-launch and
+  # fused) with the fused random-action rollout
   step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-      python bench.py --no-cpu-baseline --steps 300 --warmup 20 --policy-steps 0 --board-steps 0 ${BENCH_ARGS:-}
+      python bench.py --no-cpu-baseline --steps 300 --warmup 20 --policy-steps 0 --board-steps 0 --rollout-steps 0 ${BENCH_ARGS:-}
   find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec head -4 {} \;
   step rocprof_policy 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_policy -o run -- \
-      python bench.py --no-cpu-baseline --steps 10 --warmup 5 --policy-steps 200 --torch-policy-steps 0 --board-steps 0 ${BENCH_ARGS:-}
+      python bench.py --no-cpu-baseline --steps 10 --warmup 5 --policy-steps 200 --torch-policy-steps 0 --board-steps 0 \
+      --rollout-steps 1000 ${BENCH_ARGS:-}
   find gpurun_out/prof_${TAG}_policy -name "*kernel_stats.csv" -exec head -4 {} \;
 fi
 if [ "${PMC:-1}" = "1" ]; then
