@@ -155,3 +155,36 @@ def test_policy_rollout_generic_config(gpu):
     """An env outside the fixed shape (9 static + 4 dynamic): be_policy_rollout loops the two launches."""
     from gym_ballenv_amd.config import EnvConfig
     _policy_pair(EnvConfig(num_static=9, num_dynamic=4, time_limit=40), 2048, 10, 30, 30, True)
+
+
+def test_fused_rollouts_shard_invariance(gpu):
+    """Config 4's sharding through both fused modes: a global env's trajectory does not depend
+    on how the env batch is split over ranks (env_offset = the shard's first global env id)."""
+    from gym_ballenv_amd.config import EnvConfig
+    from gym_ballenv_amd.policy import Policy, reference_weights
+    from gym_ballenv_amd.rollout import Rollout
+    cfg = EnvConfig(time_limit=30)
+    whole = make_env(cfg, 4096, 10, gpu, seed=9)
+    parts = [make_env(cfg, n, 10, gpu, seed=9, env_offset=off) for off, n in ((0, 1024), (1024, 3072))]
+    acts_w = whole.sample_actions(40, seed=4)
+    acts_p = [p.sample_actions(40, seed=4) for p in parts]
+    np.testing.assert_array_equal(acts_w.cpu().numpy(), torch.cat(acts_p, 1).cpu().numpy())
+    for e in (whole, *parts):
+        e.reset()
+    ow, rw, dw, _ = (x.clone() if torch.is_tensor(x) else x for x in whole.rollout(acts_w))
+    res = [p.rollout(a) for p, a in zip(parts, acts_p)]
+    np.testing.assert_array_equal(ow.cpu().numpy(), torch.cat([r[0] for r in res], 1).cpu().numpy())
+    np.testing.assert_array_equal(rw.cpu().numpy(), torch.cat([r[1] for r in res], 1).cpu().numpy())
+    np.testing.assert_array_equal(dw.cpu().numpy(), torch.cat([r[2] for r in res], 1).cpu().numpy())
+    pol = Policy.from_npz(reference_weights(10), 10)
+    ros = [Rollout(e, pol, horizon=30, backend="fused", seed=0x77, chunk=30) for e in (whole, *parts)]
+    for r in ros:
+        r.run()
+    for name in ("actions", "log_probs", "values", "rewards", "dones"):
+        np.testing.assert_array_equal(getattr(ros[0], name).cpu().numpy(),
+                                      torch.cat([getattr(r, name) for r in ros[1:]], 1).cpu().numpy(), err_msg=name)
+    for r in ros:
+        r.close()
+    for e in (whole, *parts):
+        e.status()
+        e.close()
