@@ -1633,12 +1633,18 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
           load_b(tt, Ba);
           if (tt + 1 < nt && !DBG(0xF0000u)) {
             load_b(tt + 1, Bb);
-            tile_chunk2<HTC, KS, NO>(pimg, Ba, Bb, lane, h0, h1, pa, pb);
+            // chunk lengths are HT/4 or HT/4 + 1: unrolled bodies for both
+            constexpr int LS = HTC / POL_CHUNKS;
+            if (h1 - h0 == LS) tile_chunk2<HTC, KS, NO, LS>(pimg, Ba, Bb, lane, h0, h1, pa, pb);
+            else tile_chunk2<HTC, KS, NO, LS + 1>(pimg, Ba, Bb, lane, h0, h1, pa, pb);
             put(tt, pa);
             put(tt + 1, pb);
           } else {
             // (diagnostics builds: tile_chunk's own ablation bits 2 / 4 from dbg bits 17 / 18)
-            tile_chunk<HTC, KS, NO>(pimg, Ba, lane, (int)(DBG(0xF0000u) >> 16), h0, h1, pa);
+            constexpr int LS = HTC / POL_CHUNKS;
+            if (DBG(0xF0000u)) tile_chunk<HTC, KS, NO>(pimg, Ba, lane, (int)(DBG(0xF0000u) >> 16), h0, h1, pa);
+            else if (h1 - h0 == LS) tile_chunk<HTC, KS, NO, LS>(pimg, Ba, lane, 0, h0, h1, pa);
+            else tile_chunk<HTC, KS, NO, LS + 1>(pimg, Ba, lane, 0, h0, h1, pa);
             put(tt, pa);
             if (tt + 1 < nt) {
               load_b(tt + 1, Bb);

@@ -71,7 +71,7 @@ __host__ __device__ constexpr int pol_chunk_begin(int HT, int c) { return (c * H
 // One chunk [ht0, ht1) of the dense forward of a 16-env column tile (env of lane = lane & 15,
 // obs fragments B): fc1 on the int8 MFMA, relu, heads.  Returns the chunk's raw logit partials
 // (no head bias), summed over the lane groups (every lane of a column holds its env's values).
-template <int HT, int KS, int NO>
+template <int HT, int KS, int NO, int LEN = 0>
 __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS], int lane, int dbg, int ht0,
                                            int ht1, float (&out)[NO]) {
   constexpr PolLayout L = pol_layout(HT, KS, NO);
@@ -79,8 +79,11 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
   float part[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) part[o] = 0.f;
-#pragma unroll BE_POL_UNROLL
-  for (int ht = ht0; ht < ht1; ++ht) {
+  const int n = LEN > 0 ? LEN : ht1 - ht0;
+#pragma unroll
+  for (int j = 0; j < (LEN > 0 ? LEN : HT); ++j) {
+    if (LEN == 0 && j >= n) break;
+    const int ht = ht0 + j;
     v4i acc[3];   // one accumulator per digit plane: no VALU between a tile row's MFMAs
     acc[0] = v4i{0, 0, 0, 0};
     acc[1] = v4i{0, 0, 0, 0};
@@ -119,7 +122,9 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
 // tile_chunk for two tiles at once (B0, B1): the fc1 digit fragments and head weights are
 // read once for both, and the two tiles' chains interleave.  Each tile's arithmetic is
 // tile_chunk's, in the same order (bit-identical partials).
-template <int HT, int KS, int NO>
+// LEN > 0: the chunk has exactly LEN rows (fully unrolled: the loads of row j+1 can be issued
+// under row j's MFMAs); LEN == 0: a runtime trip count.
+template <int HT, int KS, int NO, int LEN = 0>
 __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[KS], const v4i (&B1)[KS], int lane,
                                             int ht0, int ht1, float (&out0)[NO], float (&out1)[NO]) {
   constexpr PolLayout L = pol_layout(HT, KS, NO);
@@ -127,7 +132,11 @@ __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[
   float p0[NO], p1[NO];
 #pragma unroll
   for (int o = 0; o < NO; ++o) { p0[o] = 0.f; p1[o] = 0.f; }
-  for (int ht = ht0; ht < ht1; ++ht) {
+  const int n = LEN > 0 ? LEN : ht1 - ht0;
+#pragma unroll
+  for (int j = 0; j < (LEN > 0 ? LEN : HT); ++j) {
+    if (LEN == 0 && j >= n) break;
+    const int ht = ht0 + j;
     v4i a0[3], a1[3];
     a0[0] = v4i{0, 0, 0, 0};
     a0[1] = v4i{0, 0, 0, 0};
@@ -167,7 +176,7 @@ __device__ __forceinline__ void tile_forward(const uint8_t* lds, const v4i (&B)[
 #pragma unroll
   for (int c = 0; c < POL_CHUNKS; ++c) {
     float part[NO];
-    tile_chunk<HT, KS, NO>(lds, B, lane, dbg, pol_chunk_begin(HT, c), pol_chunk_begin(HT, c + 1), part);
+    tile_chunk<HT, KS, NO>(lds, B, lane, dbg, pol_chunk_begin(HT, c), pol_chunk_begin(HT, c + 1), part);   // (inlined: constant bounds)
 #pragma unroll
     for (int o = 0; o < NO; ++o) out[o] = c == 0 ? part[o] : out[o] + part[o];
   }
