@@ -1582,7 +1582,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       const int c3 = s % 3;
       // the draw's uniform, a function of this env's state (in flight across the barrier)
       const float u = policy_uniform(gid, episode, (uint32_t)len, p.pol_seed);
-      if (valid && pnz) list[atomicAdd(&cnt3[c3], 1)] = (int16_t)tid;
+      int my_k = 0;   // this env's place in the list
+      if (valid && pnz) {
+        my_k = atomicAdd(&cnt3[c3], 1);
+        list[my_k] = (int16_t)tid;
+      }
       if (!DBG(DBG_POL_NO_SYNC)) __syncthreads();   // list complete (and every wave's stage rows written)
       const int cnt = cnt3[c3];
       if (tid == 0) cnt3[c3 == 0 ? 2 : c3 - 1] = 0;   // (s + 2) % 3
@@ -1654,6 +1658,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
           }
         }
         __syncthreads();   // every chunk of the round's tiles
+        if (ntiles <= NWAVE) break;   // one round (the common case): each env reads its chunks below
         if (tid < nt * 16 && r0 * 16 + tid < cnt) {   // one thread per listed env: the chunks in order
           const int e = list[r0 * 16 + tid];
           const int tt = tid >> 4, col = tid & 15;
@@ -1668,13 +1673,28 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
         __syncthreads();   // round done: pbuf free, these logits visible
       }
       static_assert(NWAVE == POL_CHUNKS, "one hidden-row chunk per wave");
-      // select_action's tail (policy_finish with the uniform drawn above)
-      const float* src = pnz ? lg + tid * NO : reinterpret_cast<const float*>(pimg + PL.table) + pquad * NO;
+      // select_action's tail (policy_finish with the uniform drawn above) on the raw logits: the
+      // chunk partials added in order (one round), the combined logits (several), or the table
+      float raw[NO];
+      if (pnz && ntiles <= NWAVE) {
+        const int tt = my_k >> 4, col = my_k & 15;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          float v = pbuf_base[((0 * NWAVE + tt) * 16 + col) * NO + o];
+#pragma unroll
+          for (int c = 1; c < NWAVE; ++c) v = v + pbuf_base[((c * NWAVE + tt) * 16 + col) * NO + o];
+          raw[o] = v;
+        }
+      } else {
+        const float* src = pnz ? lg + tid * NO : reinterpret_cast<const float*>(pimg + PL.table) + pquad * NO;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) raw[o] = src[o];
+      }
       float lp = 0.f, val = 0.f;
       if (DBG(DBG_POL_NO_FINISH)) {
         a = (int)((gid + (uint32_t)len * 7u) % 9u);
       } else {
-        const PolDist<NO> d = policy_dist<NO>(src, reinterpret_cast<const float*>(pimg + PL.hbias), p.pol_actions,
+        const PolDist<NO> d = policy_dist<NO>(raw, reinterpret_cast<const float*>(pimg + PL.hbias), p.pol_actions,
                                               nullptr);
         a = policy_pick<NO>(d.cdf, d.lp, d.last_nz, p.pol_actions, u, lp);
         val = d.value;

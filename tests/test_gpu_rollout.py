@@ -188,3 +188,32 @@ def test_fused_rollouts_shard_invariance(gpu):
     for e in (whole, *parts):
         e.status()
         e.close()
+
+
+def test_policy_rollout_crowded_multi_round(gpu):
+    """An 80x80 field: most windows are lit, so blocks list more than 4 tiles (64 envs) and the
+    fused kernel takes its multi-round path (chunk partials combined into LDS logits)."""
+    from gym_ballenv_amd.config import EnvConfig
+    from gym_ballenv_amd.policy import Policy
+    cfg = EnvConfig(screen_width=80, screen_height=80, strip_goal_x=80, strip_agent_x=80, min_spawn_dist=10.0,
+                    goals=[(12, 22), (23, 33), (47, 50), (60, 40), (30, 11)], time_limit=20)
+    torch.manual_seed(5)
+    N, T = 4096, 30
+    envs = [make_env(cfg, N, 10, "cuda:0", seed=13) for _ in range(2)]
+    from gym_ballenv_amd.rollout import Rollout
+    pol = Policy(10)
+    ros = []
+    for e, be in zip(envs, ("hip", "fused")):
+        e.reset()
+        ros.append(Rollout(e, pol, horizon=T, backend=be, record_obs=True, seed=3, chunk=T))
+    for r in ros:
+        r.run_eager()
+    for name in ("actions", "log_probs", "values", "rewards", "dones", "obs"):
+        np.testing.assert_array_equal(getattr(ros[1], name).cpu().numpy(), getattr(ros[0], name).cpu().numpy(),
+                                      err_msg=name)
+    lit = (ros[0].obs[:T, :, 4:].amax(-1) > 0).reshape(T, N // 256, 256).sum(-1)
+    assert int(lit.max()) > 64, int(lit.max())   # the multi-round path ran
+    for r, e in zip(ros, envs):
+        e.status()
+        r.close()
+        e.close()
