@@ -30,9 +30,10 @@
 // 115-130, 170-193).  The kernel computes those terms from that identity.
 //
 // One lane per env; the env index is the unit-stride HBM axis of every array.  Resets
-// (reset(), or autoreset inside step) run on the env's own lane: sequential draws from a
-// tape (parity mode: the reference's ranf/randint values in call order) or Philox(seed;
-// gid, episode, 0, BOARD<<24 | block).
+// (reset(), or autoreset inside step) draw from a tape on the env's own lane (parity mode:
+// the reference's ranf/randint values in call order), or from Philox(seed; gid, episode, 0,
+// BOARD<<24 | sub), wave-cooperatively (wave_board_resets: every rejection loop becomes one
+// ballot over 64 candidate attempts).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -121,19 +122,23 @@ __device__ void features(const BParams& p, int i, double ax, double ay, double g
   else if (ang > PI / 4 && ang < PI * 3 / 4) { if (vx > 0) f[2] = 1.f; else f[4] = 1.f; }
   else f[3] = 1.f;
   // density (:91-112), speed/orientation (:115-130), social forces (:170-193)
+  // branch-free over the MAXS slots (slots past ns are masked out), so the obstacles' f64
+  // chains (sqrt, exp) interleave; the sums keep the reference's obstacle order
   double sf = 0.0;
 #pragma unroll
   for (int k = 0; k < MAXS; ++k) {
-    if (k >= p.ns) break;
+    const bool real = k < p.ns;
     const int32_t o = so[k];
     const double ox = (double)sx(o), oy = (double)sy(o);
     const double N = dist2(ox, oy, ax, ay) - p.r_agent - p.r_feature_obs;   // calcDistance
-    if (N < 1000.0) f[7] += 1.f;
-    if (N < 230.0) f[6] += 1.f;
-    if (N < 101.0) f[5] += 1.f;
-    f[8 + 3 * 1 + 0] += 1.f;                           // orientation bin 1, speed bin 0
-    const double fsoc = exp(-N / 10.0) * N * 1.5;      // a*exp(-N/b)*N*thrPart, a = 1, b = 10
-    if (fsoc > 1.0) sf += fsoc;                        // -> phi_SF[orientation bin 1]
+    f[7] += (real && N < 1000.0) ? 1.f : 0.f;
+    f[6] += (real && N < 230.0) ? 1.f : 0.f;
+    f[5] += (real && N < 101.0) ? 1.f : 0.f;
+    f[8 + 3 * 1 + 0] += real ? 1.f : 0.f;              // orientation bin 1, speed bin 0
+    // a*exp(-N/b)*N*thrPart, a = 1, b = 10; -N*0.1 is within an ulp of -N/10 (exp's own
+    // accuracy class; only sf's f32 value and its > 1 cut, a measure-zero boundary, see it)
+    const double fsoc = exp(N * -0.1) * N * 1.5;
+    sf += (real && fsoc > 1.0) ? fsoc : 0.0;           // -> phi_SF[orientation bin 1]
   }
   f[17 + 1] = (float)sf;
   float4* row = reinterpret_cast<float4*>(p.features + (int64_t)i * 20);   // 80-B rows: 5 x 16 B
@@ -178,21 +183,117 @@ __device__ void reset_env(const BParams& p, int i, uint32_t episode, double& ax,
   total = dist2(ax, ay, gx, gy);                                 // total_distance
 }
 
+// Philox-mode resets, wave-cooperative: the wave's finished envs (mask m) are reset one after
+// the other by all 64 lanes.  Lane r draws agent attempt r, and lane a*ns + k draws attempt a
+// of static k, so the reference's rejection loops (the first accepted attempt, in attempt
+// order) become a ballot instead of a serial chain on one lane.  Counter layout (purpose 6,
+// c1 = the new episode): sub 0 = the goal, 1<<20 | r = agent attempt r, 2<<20 | k<<12 | a =
+// static k attempt a; ranf = 53 bits from two words, randint = multiply-shift of one.
+__device__ __forceinline__ double ranf2(uint32_t w0, uint32_t w1) {
+  return ((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+template <int MAXS>
+__device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32_t gid, uint32_t episode_new,
+                                  double& ax, double& ay, double& gx, double& gy, double& d0, double& total,
+                                  int32_t (&so)[MAXS]) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int ns = p.ns;
+  const int per = ns > 0 ? 64 / ns : 64;   // static attempts per pass
+  while (m) {
+    const int l = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)gid, l);
+    const uint32_t ep = (uint32_t)__builtin_amdgcn_readlane((int)episode_new, l);
+    // goal (every lane: same block), agent attempts r0 + lane (ballenv_pygame.py:462-470)
+    const u4 bg = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, 0u), p.seed);
+    const double rgx = (double)(p.W - p.sgx) + ranf2(bg.x, bg.y) * (double)p.sgx;
+    const double rgy = (double)(p.H - p.sgy) + ranf2(bg.z, bg.w) * (double)p.sgy;
+    double rax = 0.0, ray = 0.0, rd0 = 0.0;
+    for (int r0 = 0;; r0 += 64) {
+      const u4 ba = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (1u << 20) | (uint32_t)(r0 + lane)), p.seed);
+      const double cx = ranf2(ba.x, ba.y) * (double)p.sax, cy = ranf2(ba.z, ba.w) * (double)p.say;
+      const double dc = dist2(rgx, rgy, cx, cy);
+      if (r0 == 0) rd0 = readlane_f64(dc, 0);                     // state[2]: the first distance
+      const unsigned long long ok = __ballot(!(dc < p.min_spawn));
+      if (ok || r0 + 64 > BOARD_REJECT_LIMIT) {
+        if (!ok) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+        const int q = ok ? __ffsll((long long)ok) - 1 : 63;
+        rax = readlane_f64(cx, q); ray = readlane_f64(cy, q);
+        break;
+      }
+    }
+    // statics (:489-498): lane = a * ns + k, the first accepted attempt of each k
+    const int k_l = ns > 0 ? lane % ns : 0, a_l = ns > 0 ? lane / ns : 0;
+    const bool in_pass = ns > 0 && a_l < per;
+    int32_t cand = 0;
+    unsigned long long need = ns > 0 ? ((ns >= 64 ? ~0ull : (1ull << ns) - 1)) : 0ull;   // statics still open
+    int32_t got[MAXS];
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k) got[k] = 0;
+    for (int a0 = 0; need; a0 += per) {
+      bool ok = false;
+      if (in_pass) {
+        const u4 bo = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (2u << 20) | ((uint32_t)k_l << 12) | (uint32_t)(a0 + a_l)),
+                             p.seed);
+        const int ox = p.sox + (int)__umulhi(bo.x, (uint32_t)(p.W - 2 * p.sox));
+        const int oy = p.soy + (int)__umulhi(bo.y, (uint32_t)(p.H - 2 * p.soy));
+        ok = dist2((double)ox, (double)oy, rax, ray) - p.thr_agent > p.r_collide &&
+             dist2((double)ox, (double)oy, rgx, rgy) - p.thr_goal > p.r_collide;
+        cand = (int32_t)(((uint32_t)ox & 0xFFFFu) | ((uint32_t)oy << 16));
+      }
+      const unsigned long long okm = __ballot(ok);
+      const bool give_up = a0 + per > BOARD_REJECT_LIMIT;
+#pragma unroll
+      for (int k = 0; k < MAXS; ++k) {
+        if (k >= ns || !((need >> k) & 1ull)) continue;
+        // lanes of static k: k, k + ns, k + 2 ns, ... (attempt order)
+        unsigned long long km = 0;
+        for (int a = 0; a < per; ++a) km |= 1ull << (a * ns + k);
+        const unsigned long long hit = okm & km;
+        if (hit || give_up) {
+          if (!hit && lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+          got[k] = __builtin_amdgcn_readlane(cand, hit ? __ffsll((long long)hit) - 1 : k);
+          need &= ~(1ull << k);
+        }
+      }
+    }
+    if (lane == l) {
+      gx = rgx; gy = rgy; ax = rax; ay = ray; d0 = rd0;
+      total = dist2(rax, ray, rgx, rgy);                           // total_distance
+#pragma unroll
+      for (int k = 0; k < MAXS; ++k) so[k] = got[k];
+    }
+  }
+}
+
 // MAXS: compile-time bound on the static-obstacle count (8 / 16 / 32), so the obstacle
 // loops unroll with a runtime guard and the positions stay in registers (no scratch).
 template <int MAXS>
 __global__ __launch_bounds__(256) void board_kernel(BParams p) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= p.n) return;
+  // every lane of a wave stays to the end (the Philox resets are wave-cooperative); lanes past
+  // N work on a clamped index and store nothing
+  const int i0 = blockIdx.x * 256 + threadIdx.x;
+  const bool valid = i0 < p.n;
+  const int i = valid ? i0 : p.n - 1;
   int32_t so[MAXS];
 #pragma unroll
   for (int k = 0; k < MAXS; ++k) so[k] = k < p.ns ? p.statics[(int64_t)k * p.n + i] : 0;
   const double2 ag = reinterpret_cast<const double2*>(p.agent)[i];
   const double2 gl = reinterpret_cast<const double2*>(p.goal)[i];
   double ax = ag.x, ay = ag.y, gx = gl.x, gy = gl.y;
-  if (p.mode == 2) { features(p, i, ax, ay, gx, gy, so); return; }
+  if (p.mode == 2) {
+    if (valid) features(p, i, ax, ay, gx, gy, so);
+    return;
+  }
   uint32_t episode = p.episode[i];
-  bool do_reset = p.mode == 1 && (!p.mask || p.mask[i]);
+  bool do_reset = valid && p.mode == 1 && (!p.mask || p.mask[i]);
   double total = p.total[i], ret = p.ep_return[i], dist = p.dist[i];
   int32_t len = p.ep_len[i];
   if (p.mode == 0) {
@@ -217,21 +318,29 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     bool done = false;
 #pragma unroll
     for (int k = 0; k < MAXS; ++k)   // any hit (the reference stops at the first; the result is the same)
-      done = done || (k < p.ns && !(dist2(ax, ay, (double)sx(so[k]), (double)sy(so[k])) > p.r_collide));
+      done |= (k < p.ns) & !(dist2(ax, ay, (double)sx(so[k]), (double)sy(so[k])) > p.r_collide);
     if (done) { r = -1.0; ret += -1.0; }
     else if (dist < p.goal_thr) { done = true; r = 1.0; ret += 1.0; }
     else { r = (old - dist) / total; ret += r; }
     ++len;
     const bool trunc = !done && p.time_limit > 0 && len >= p.time_limit;
     done = done || trunc;
-    p.reward[i] = r;
-    p.done[i] = done ? 1 : 0;
-    if (p.truncated) p.truncated[i] = trunc ? 1 : 0;
-    do_reset = done && p.autoreset;
+    if (valid) {
+      p.reward[i] = r;
+      p.done[i] = done ? 1 : 0;
+      if (p.truncated) p.truncated[i] = trunc ? 1 : 0;
+    }
+    do_reset = valid && done && p.autoreset;
   }
+  if (p.tape) {   // parity mode: the reference's draw order, on the env's own lane
+    if (do_reset) reset_env(p, i, episode + 1u, ax, ay, gx, gy, dist, total, so);
+  } else {
+    const unsigned long long m = __ballot(do_reset);
+    if (m) wave_board_resets<MAXS>(p, m, (uint32_t)p.gid0 + (uint32_t)i, episode + 1u, ax, ay, gx, gy, dist, total, so);
+  }
+  if (!valid) return;
   if (do_reset) {
     ++episode;
-    reset_env(p, i, episode, ax, ay, gx, gy, dist, total, so);
     ret = 0.0; len = 0;
 #pragma unroll
     for (int k = 0; k < MAXS; ++k)
@@ -365,7 +474,13 @@ static int board_launch(be_board* b, const be_board_state* st, const be_board_ou
   p.r_collide = c.static_radius + c.agent_radius; p.r_feature_obs = c.obstacle_feature_radius;
   p.r_agent = c.agent_radius; p.goal_thr = c.goal_threshold; p.min_spawn = c.min_spawn_dist;
   p.thr_agent = c.spawn_thresh_agent; p.thr_goal = c.spawn_thresh_goal;
-  void (*fn)(BParams) = c.num_static <= 8 ? board_kernel<8> : (c.num_static <= 16 ? board_kernel<16> : board_kernel<32>);
+  // the obstacle loops run MAXS slots branch-free: the smallest bound that covers num_static
+  void (*fn)(BParams) = c.num_static <= 4    ? board_kernel<4>
+                        : c.num_static <= 6  ? board_kernel<6>
+                        : c.num_static <= 8  ? board_kernel<8>
+                        : c.num_static <= 12 ? board_kernel<12>
+                        : c.num_static <= 16 ? board_kernel<16>
+                                             : board_kernel<32>;
   hipLaunchKernelGGL(fn, dim3((unsigned)((c.num_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p);
   e = hipGetLastError();
   if (e != hipSuccess) return bhip(b, e);
