@@ -1623,17 +1623,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
             Bt[ks] = v;
           }
         };
-        auto put = [&](int tt, const float (&part)[NO]) {
-          if (g4 == 0) {
+        auto put = [&](int tt, const float (&part)[PolQ<NO>::N]) {   // lane group g4: outputs g4, g4 + 4, ...
 #pragma unroll
-            for (int o = 0; o < NO; ++o) pbuf[((w * NWAVE + tt) * 16 + lane) * NO + o] = part[o];
-          }
+          for (int q = 0; q < PolQ<NO>::N; ++q)
+            if (4 * q + g4 < NO) pbuf[((w * NWAVE + tt) * 16 + (lane & 15)) * NO + 4 * q + g4] = part[q];
         };
         constexpr int HTC = HT > 0 ? HT : 1;
         const int h0 = pol_chunk_begin(HTC, w), h1 = pol_chunk_begin(HTC, w + 1);
         for (int tt = 0; tt < nt; tt += 2) {   // two tiles at a time: shared weight reads, interleaved chains
           v4i Ba[KS], Bb[KS];
-          float pa[NO], pb[NO];
+          float pa[PolQ<NO>::N], pb[PolQ<NO>::N];
           load_b(tt, Ba);
           if (tt + 1 < nt && !DBG(0xF0000u)) {
             load_b(tt + 1, Bb);

@@ -49,6 +49,29 @@ __device__ __forceinline__ float sum_groups(float x) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// sum_groups of four values at once: lane group (row) r gets the full sum of value r, each
+// added in sum_groups' order ((g0 + g1) + (g2 + g3)) -- two permlane16 swaps pair the values'
+// rows, one permlane32 swap finishes all four (6 instructions instead of 16).
+__device__ __forceinline__ float sum_groups4(float x0, float x1, float x2, float x3) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
+  const float c = __uint_as_float(a[0]) + __uint_as_float(a[1]);   // rows: x0 01, x1 01, x0 23, x1 23
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x2), __float_as_uint(x3), false, false);
+  const float e = __uint_as_float(b[0]) + __uint_as_float(b[1]);   // rows: x2 01, x3 01, x2 23, x3 23
+  const auto d = __builtin_amdgcn_permlane32_swap(__float_as_uint(c), __float_as_uint(e), false, false);
+  return __uint_as_float(d[0]) + __uint_as_float(d[1]);
+}
+
+// A tile's NO outputs in NQ = ceil(NO/4) registers: register q of lane group g holds output 4q + g.
+template <int NO> struct PolQ { static constexpr int N = (NO + 3) / 4; };
+template <int NO>
+__device__ __forceinline__ void sum_outputs(const float (&part)[NO], float (&out)[PolQ<NO>::N]) {
+#pragma unroll
+  for (int q = 0; q < PolQ<NO>::N; ++q) {
+    auto at = [&](int o) { return o < NO ? part[o] : 0.f; };
+    out[q] = sum_groups4(at(4 * q), at(4 * q + 1), at(4 * q + 2), at(4 * q + 3));
+  }
+}
+
 #ifndef BE_POL_UNROLL
 #define BE_POL_UNROLL 13
 #endif
@@ -70,10 +93,11 @@ __host__ __device__ constexpr int pol_chunk_begin(int HT, int c) { return (c * H
 
 // One chunk [ht0, ht1) of the dense forward of a 16-env column tile (env of lane = lane & 15,
 // obs fragments B): fc1 on the int8 MFMA, relu, heads.  Returns the chunk's raw logit partials
-// (no head bias), summed over the lane groups (every lane of a column holds its env's values).
+// (no head bias), summed over the lane groups, in PolQ layout: register q of lane group g holds
+// output 4q + g of the env of column lane & 15.
 template <int HT, int KS, int NO, int LEN = 0>
 __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS], int lane, int dbg, int ht0,
-                                           int ht1, float (&out)[NO]) {
+                                           int ht1, float (&out)[PolQ<NO>::N]) {
   constexpr PolLayout L = pol_layout(HT, KS, NO);
   const int g = lane >> 4;
   float part[NO];
@@ -115,8 +139,7 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
       part[0] += h[0] + h[1] + h[2] + h[3];
     }
   }
-#pragma unroll
-  for (int o = 0; o < NO; ++o) out[o] = sum_groups(part[o]);
+  sum_outputs<NO>(part, out);
 }
 
 // tile_chunk for two tiles at once (B0, B1): the fc1 digit fragments and head weights are
@@ -126,7 +149,8 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
 // under row j's MFMAs); LEN == 0: a runtime trip count.
 template <int HT, int KS, int NO, int LEN = 0>
 __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[KS], const v4i (&B1)[KS], int lane,
-                                            int ht0, int ht1, float (&out0)[NO], float (&out1)[NO]) {
+                                            int ht0, int ht1, float (&out0)[PolQ<NO>::N],
+                                            float (&out1)[PolQ<NO>::N]) {
   constexpr PolLayout L = pol_layout(HT, KS, NO);
   const int g = lane >> 4;
   float p0[NO], p1[NO];
@@ -165,20 +189,20 @@ __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[
       p1[o] = fmaf(w.w, h1[3], fmaf(w.z, h1[2], fmaf(w.y, h1[1], fmaf(w.x, h1[0], p1[o]))));
     }
   }
-#pragma unroll
-  for (int o = 0; o < NO; ++o) { out0[o] = sum_groups(p0[o]); out1[o] = sum_groups(p1[o]); }
+  sum_outputs<NO>(p0, out0);
+  sum_outputs<NO>(p1, out1);
 }
 
 // The whole dense forward of one tile on one wave: the four chunks in order.
 template <int HT, int KS, int NO>
 __device__ __forceinline__ void tile_forward(const uint8_t* lds, const v4i (&B)[KS], int lane, int dbg,
-                                             float (&out)[NO]) {
+                                             float (&out)[PolQ<NO>::N]) {
 #pragma unroll
   for (int c = 0; c < POL_CHUNKS; ++c) {
-    float part[NO];
+    float part[PolQ<NO>::N];
     tile_chunk<HT, KS, NO>(lds, B, lane, dbg, pol_chunk_begin(HT, c), pol_chunk_begin(HT, c + 1), part);   // (inlined: constant bounds)
 #pragma unroll
-    for (int o = 0; o < NO; ++o) out[o] = c == 0 ? part[o] : out[o] + part[o];
+    for (int q = 0; q < PolQ<NO>::N; ++q) out[q] = c == 0 ? part[q] : out[q] + part[q];
   }
 }
 
