@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--cpu-procs", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph-chunk", type=int, default=250, help="steps per captured graph")
-    p.add_argument("--policy-steps", type=int, default=200,
+    p.add_argument("--policy-steps", type=int, default=1000,
                    help="config 5 leg: timed steps of the on-GPU policy rollout (0 = skip)")
     p.add_argument("--torch-policy-steps", type=int, default=50,
                    help="config 5 comparison: timed steps with the PyTorch-ROCm policy (0 = skip)")
@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="N > 1 collective backend (nccl = RCCL over xGMI); gloo only to rehearse the "
                         "multi-rank path with several ranks sharing one GPU")
-    p.add_argument("--board-steps", type=int, default=200,
+    p.add_argument("--board-steps", type=int, default=1000,
                    help="createBoard profile leg (SURVEY 8(f) rank 2): timed steps (0 = skip)")
     return p.parse_args()
 

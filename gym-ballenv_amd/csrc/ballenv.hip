@@ -1562,7 +1562,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   const Win g0(p, 0, 0);
   const uint32_t R2 = (uint32_t)g0.R2;
   const NearBox nb0(g0);
-  const int bxo = p.speed_x * (p.window / 2) + g0.R, byo = p.speed_y * (p.window / 2) + g0.R;
+  const int bxo = WT / 2 + g0.R, byo = WT / 2 + g0.R;   // unit speeds
   typedef unsigned short v2u __attribute__((ext_vector_type(2)));
   const v2s boxo = {(short)bxo, (short)byo};
   const v2u boxw = {(unsigned short)nb0.bw, (unsigned short)nb0.bh};
@@ -1709,8 +1709,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
     const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
     const int dx = (int)((p.amx >> sh) & 3u) - 1, dy = (int)((p.amy >> sh) & 3u) - 1;
-    ax = min(max(ax + p.speed_x * dx, 0), p.screen_w);
-    ay = min(max(ay + p.speed_y * dy, 0), p.screen_h);
+    ax = min(max(ax + dx, 0), p.screen_w);   // unit speeds (pick_rollout's precondition)
+    ay = min(max(ay + dy, 0), p.screen_h);
     bool hs = false, hd = false;
     nl.cnt = 0;
     // ---- dynamic obstacles (counter == ep_len mod (G+1): all start at 0 on reset)
