@@ -302,6 +302,36 @@ def board_leg(args, gb, dev, rank, world, stream):
            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
            "kernel_us_mean": ms * 1e3, "bytes_per_env_step": B, "achieved_GBs": B * N / (ms * 1e-3) / 1e9}
     del g
+    # the same rollout fused: be_board_rollout, 100 steps per launch with the state in registers
+    Kc = min(100, T)
+    b.rollout(acts[:Kc])                            # warm-up; allocates the (Kc, N, ...) buffers
+    f, r, dn, info = b.rollout(acts[:Kc])
+    out = gb._abi.BeBoardOut(f.data_ptr(), r.data_ptr(), dn.data_ptr(), info["truncated"].data_ptr())
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    sp = C.c_void_p(stream.cuda_stream)
+    for c0 in range(0, T - T % Kc, Kc):
+        lib.be_board_rollout(b._h, C.byref(b._st), C.c_void_p(acts[c0].data_ptr()), None, Kc, C.byref(out), sp)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    Tf = T - T % Kc
+    b.status()
+    res["fused"] = {"what": f"be_board_rollout, {Kc} steps per launch (state in registers; per-step features, "
+                            "reward, done, truncated to (K, N, ...) buffers; bit-identical to be_board_step)",
+                    "value": Tf * N * world / el, "unit": "env-steps/s", "ms_per_step": el / Tf * 1e3,
+                    "kernel_us_per_step": ev0.elapsed_time(ev1) * 1e3 / Tf}
     b.close()
     return res
 

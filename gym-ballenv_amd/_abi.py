@@ -28,7 +28,7 @@ EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_by
            "be_status", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
            "be_policy_rollout", "be_policy_bytes", "be_observe_blocks",
            "be_board_config_default", "be_board_create", "be_board_destroy", "be_board_last_error",
-           "be_board_reset", "be_board_step", "be_board_observe", "be_board_status")
+           "be_board_reset", "be_board_step", "be_board_rollout", "be_board_observe", "be_board_status")
 BOARD_MAX_STATIC, BOARD_MAX_ACTIONS, BOARD_FEATURES = 32, 16, 20
 
 
@@ -138,6 +138,7 @@ def lib() -> C.CDLL:
         "be_board_last_error": (C.c_char_p, [vp]),
         "be_board_reset": (C.c_int, [vp, P(BeBoardState), vp, vp, i32, P(BeBoardOut), vp]),
         "be_board_step": (C.c_int, [vp, P(BeBoardState), vp, vp, P(BeBoardOut), vp]),
+        "be_board_rollout": (C.c_int, [vp, P(BeBoardState), vp, vp, i32, P(BeBoardOut), vp]),
         "be_board_observe": (C.c_int, [vp, P(BeBoardState), P(BeBoardOut), vp]),
         "be_board_status": (C.c_int, [vp, P(i32), vp]),
     }

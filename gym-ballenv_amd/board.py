@@ -104,6 +104,39 @@ class BatchedBoard:
         self._keep = (a, d)
         return self.features, self.reward, self.done, {"truncated": self.truncated}
 
+    def rollout(self, actions: Optional[torch.Tensor] = None, deltas: Optional[torch.Tensor] = None):
+        """K steps in one launch (be_board_rollout): actions (K, N) indices or deltas (K, N, 2).
+        Returns per-step (features (K, N, 20), reward (K, N), done (K, N), info{truncated}),
+        exactly what K step() calls return, stacked.  The buffers are reused by the next
+        rollout of the same K."""
+        a = d = None
+        if actions is not None:
+            a = actions.to(device=self.device, dtype=torch.uint8).contiguous()
+            K = a.shape[0]
+            if a.dim() != 2 or a.shape[1] != self.num_envs:
+                raise ValueError(f"actions must be (K, {self.num_envs})")
+        elif deltas is not None:
+            d = deltas.to(device=self.device, dtype=torch.float64).contiguous()
+            K = d.shape[0]
+            if d.dim() != 3 or d.shape[1:] != (self.num_envs, 2):
+                raise ValueError(f"deltas must be (K, {self.num_envs}, 2)")
+        else:
+            raise ValueError("rollout needs actions or deltas")
+        N = self.num_envs
+        buf = getattr(self, "_ro_buf", None)
+        if buf is None or buf[0].shape[0] != K:
+            z = lambda *shape, dt: torch.zeros(*shape, dtype=dt, device=self.device)  # noqa: E731
+            buf = (z(K, N, _abi.BOARD_FEATURES, dt=torch.float32), z(K, N, dt=torch.float64), z(K, N, dt=torch.bool),
+                   z(K, N, dt=torch.bool))
+            self._ro_buf = buf
+        f, r, dn, tr = buf
+        out = _abi.BeBoardOut(f.data_ptr(), r.data_ptr(), dn.data_ptr(), tr.data_ptr())
+        _abi.board_check(self._lib.be_board_rollout(self._h, C.byref(self._st), None if a is None else a.data_ptr(),
+                                                    None if d is None else d.data_ptr(), int(K), C.byref(out),
+                                                    self._stream()), self._h)
+        self._keep = (a, d)
+        return f, r, dn, {"truncated": tr}
+
     def observe(self) -> torch.Tensor:
         _abi.board_check(self._lib.be_board_observe(self._h, C.byref(self._st), C.byref(self._out), self._stream()),
                          self._h)

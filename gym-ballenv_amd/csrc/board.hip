@@ -64,7 +64,8 @@ struct BParams {
   const BoardTables* tables;
   int* status;
   unsigned long long seed;
-  int32_t n, ns, num_actions, time_limit, autoreset, gid0, mode;   // mode: 0 step, 1 reset, 2 observe
+  int32_t n, ns, num_actions, time_limit, autoreset, gid0, mode;   // mode: 0 step, 1 reset, 2 observe, 3 rollout
+  int32_t steps;                                                   // mode 3
   int32_t W, H, sox, soy, sgx, sgy, sax, say;
   double r_collide, r_feature_obs, r_agent, goal_thr, min_spawn, thr_agent, thr_goal;
 };
@@ -105,7 +106,7 @@ struct Draws {
 
 // featureExtractor(state, obstacle_list, (0, 0), agent_rad) -> 20 f32 (featureExtractor.py:247-265)
 template <int MAXS>
-__device__ void features(const BParams& p, int i, double ax, double ay, double gx, double gy, const int32_t (&so)[MAXS]) {
+__device__ void features(const BParams& p, int64_t i, double ax, double ay, double gx, double gy, const int32_t (&so)[MAXS]) {
   float f[20];
 #pragma unroll
   for (int k = 0; k < 20; ++k) f[k] = 0.f;
@@ -275,7 +276,7 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
 
 // MAXS: compile-time bound on the static-obstacle count (8 / 16 / 32), so the obstacle
 // loops unroll with a runtime guard and the positions stay in registers (no scratch).
-template <int MAXS>
+template <int MAXS, bool ROLL = false>
 __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   // every lane of a wave stays to the end (the Philox resets are wave-cooperative); lanes past
   // N work on a clamped index and store nothing
@@ -293,55 +294,66 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     return;
   }
   uint32_t episode = p.episode[i];
-  bool do_reset = valid && p.mode == 1 && (!p.mask || p.mask[i]);
   double total = p.total[i], ret = p.ep_return[i], dist = p.dist[i];
   int32_t len = p.ep_len[i];
-  if (p.mode == 0) {
-    double dx = 0.0, dy = 0.0;
-    if (p.actions) {
-      int a = p.actions[i];
-      if (a >= p.num_actions) { atomicOr(p.status, BE_STATUS_BAD_ACTION); a = 0; }
-      dx = p.tables->actions[a][0]; dy = p.tables->actions[a][1];
-    } else {
-      dx = p.deltas[2 * (int64_t)i]; dy = p.deltas[2 * (int64_t)i + 1];
-    }
-    const double old = dist2(ax, ay, gx, gy);                    // self.old_dist (:652)
-    double nx = ax + dx, ny = ay + dy;
-    if (nx < 0) nx = 0;
-    if (nx > p.W) nx = p.W;
-    if (ny < 0) ny = 0;
-    if (ny > p.H) ny = p.H;
-    ax = nx; ay = ny;
-    dist = dist2(ax, ay, gx, gy);                                // state[2] (:668)
-    // calc_reward (:680-706)
-    double r;
-    bool done = false;
+  bool was_reset = false;   // goal / total / episode / statics changed: store them at the end
+  // mode 3 (be_board_rollout): p.steps steps with the state in registers, per-step outputs in
+  // (steps, N, ...) rows; modes 0 / 1 are one pass of the same body
+  const int steps = ROLL ? p.steps : 1;   // ROLL: the mode-3 instantiation
+  for (int s = 0; s < steps; ++s) {
+    const int64_t row = (int64_t)s * p.n + i;   // this step's output row (i for modes 0 / 1)
+    bool do_reset = valid && p.mode == 1 && (!p.mask || p.mask[i]);
+    if (p.mode != 1) {
+      double dx = 0.0, dy = 0.0;
+      if (p.actions) {
+        int a = p.actions[row];
+        if (a >= p.num_actions) { atomicOr(p.status, BE_STATUS_BAD_ACTION); a = 0; }
+        dx = p.tables->actions[a][0]; dy = p.tables->actions[a][1];
+      } else {
+        dx = p.deltas[2 * row]; dy = p.deltas[2 * row + 1];
+      }
+      const double old = dist2(ax, ay, gx, gy);                    // self.old_dist (:652)
+      double nx = ax + dx, ny = ay + dy;
+      if (nx < 0) nx = 0;
+      if (nx > p.W) nx = p.W;
+      if (ny < 0) ny = 0;
+      if (ny > p.H) ny = p.H;
+      ax = nx; ay = ny;
+      dist = dist2(ax, ay, gx, gy);                                // state[2] (:668)
+      // calc_reward (:680-706)
+      double r;
+      bool done = false;
 #pragma unroll
-    for (int k = 0; k < MAXS; ++k)   // any hit (the reference stops at the first; the result is the same)
-      done |= (k < p.ns) & !(dist2(ax, ay, (double)sx(so[k]), (double)sy(so[k])) > p.r_collide);
-    if (done) { r = -1.0; ret += -1.0; }
-    else if (dist < p.goal_thr) { done = true; r = 1.0; ret += 1.0; }
-    else { r = (old - dist) / total; ret += r; }
-    ++len;
-    const bool trunc = !done && p.time_limit > 0 && len >= p.time_limit;
-    done = done || trunc;
-    if (valid) {
-      p.reward[i] = r;
-      p.done[i] = done ? 1 : 0;
-      if (p.truncated) p.truncated[i] = trunc ? 1 : 0;
+      for (int k = 0; k < MAXS; ++k)   // any hit (the reference stops at the first; the result is the same)
+        done |= (k < p.ns) & !(dist2(ax, ay, (double)sx(so[k]), (double)sy(so[k])) > p.r_collide);
+      if (done) { r = -1.0; ret += -1.0; }
+      else if (dist < p.goal_thr) { done = true; r = 1.0; ret += 1.0; }
+      else { r = (old - dist) / total; ret += r; }
+      ++len;
+      const bool trunc = !done && p.time_limit > 0 && len >= p.time_limit;
+      done = done || trunc;
+      if (valid) {
+        p.reward[row] = r;
+        p.done[row] = done ? 1 : 0;
+        if (p.truncated) p.truncated[row] = trunc ? 1 : 0;
+      }
+      do_reset = valid && done && p.autoreset;
     }
-    do_reset = valid && done && p.autoreset;
-  }
-  if (p.tape) {   // parity mode: the reference's draw order, on the env's own lane
-    if (do_reset) reset_env(p, i, episode + 1u, ax, ay, gx, gy, dist, total, so);
-  } else {
-    const unsigned long long m = __ballot(do_reset);
-    if (m) wave_board_resets<MAXS>(p, m, (uint32_t)p.gid0 + (uint32_t)i, episode + 1u, ax, ay, gx, gy, dist, total, so);
+    if (p.tape) {   // parity mode: the reference's draw order, on the env's own lane
+      if (do_reset) reset_env(p, i, episode + 1u, ax, ay, gx, gy, dist, total, so);
+    } else {
+      const unsigned long long m = __ballot(do_reset);
+      if (m) wave_board_resets<MAXS>(p, m, (uint32_t)p.gid0 + (uint32_t)i, episode + 1u, ax, ay, gx, gy, dist, total, so);
+    }
+    if (do_reset) {
+      ++episode;
+      ret = 0.0; len = 0;
+      was_reset = true;
+    }
+    if (valid && p.features) features(p, row, ax, ay, gx, gy, so);
   }
   if (!valid) return;
-  if (do_reset) {
-    ++episode;
-    ret = 0.0; len = 0;
+  if (was_reset) {
 #pragma unroll
     for (int k = 0; k < MAXS; ++k)
       if (k < p.ns) p.statics[(int64_t)k * p.n + i] = so[k];
@@ -353,7 +365,6 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   p.dist[i] = dist;
   p.ep_return[i] = ret;
   p.ep_len[i] = len;
-  if (p.features) features(p, i, ax, ay, gx, gy, so);
 }
 
 }  // namespace
@@ -445,14 +456,18 @@ const char* be_board_last_error(const be_board* b) { return b ? b->err : g_board
 
 static int board_launch(be_board* b, const be_board_state* st, const be_board_out* out, int mode,
                         const uint8_t* actions, const double* deltas, const uint8_t* mask, const double* tape,
-                        int32_t tape_len, void* stream) {
+                        int32_t tape_len, void* stream, int32_t steps = 1) {
   if (!b) return bfail(nullptr, BE_E_INVALID, "board is NULL");
   if (!st || !st->agent || !st->goal || !st->dist || !st->total_dist || !st->ep_return || !st->ep_len ||
       !st->episode || (b->cfg.num_static > 0 && !st->static_obs))
     return bfail(b, BE_E_INVALID, "be_board_state has a NULL pointer");
   if (!out) return bfail(b, BE_E_INVALID, "out is NULL");
-  if (mode == 0 && (!out->reward || !out->done)) return bfail(b, BE_E_INVALID, "be_board_step needs out->reward and out->done");
-  if (mode == 0 && !actions && !deltas) return bfail(b, BE_E_INVALID, "be_board_step needs actions or deltas");
+  if ((mode == 0 || mode == 3) && (!out->reward || !out->done))
+    return bfail(b, BE_E_INVALID, "be_board_step / be_board_rollout need out->reward and out->done");
+  if ((mode == 0 || mode == 3) && !actions && !deltas)
+    return bfail(b, BE_E_INVALID, "be_board_step / be_board_rollout need actions or deltas");
+  if (mode == 3 && steps < 0) return bfail(b, BE_E_INVALID, "steps < 0");
+  if (mode == 3 && steps == 0) return BE_OK;
   if (mode == 2 && !out->features) return bfail(b, BE_E_INVALID, "be_board_observe needs out->features");
   if (tape && tape_len < 0) return bfail(b, BE_E_INVALID, "tape_len < 0");
   int cur = -1;
@@ -468,19 +483,28 @@ static int board_launch(be_board* b, const be_board_state* st, const be_board_ou
   p.actions = actions; p.deltas = deltas; p.mask = mask; p.tape = tape; p.tape_len = tape ? tape_len : 0;
   p.tables = b->d_tables; p.status = b->status; p.seed = c.seed;
   p.n = c.num_envs; p.ns = c.num_static; p.num_actions = c.num_actions; p.time_limit = c.time_limit;
-  p.autoreset = c.autoreset; p.gid0 = (int32_t)(uint32_t)c.env_offset; p.mode = mode;
+  p.autoreset = c.autoreset; p.gid0 = (int32_t)(uint32_t)c.env_offset; p.mode = mode; p.steps = steps;
   p.W = c.screen_width; p.H = c.screen_height; p.sox = c.strip_obs_x; p.soy = c.strip_obs_y;
   p.sgx = c.strip_goal_x; p.sgy = c.strip_goal_y; p.sax = c.strip_agent_x; p.say = c.strip_agent_y;
   p.r_collide = c.static_radius + c.agent_radius; p.r_feature_obs = c.obstacle_feature_radius;
   p.r_agent = c.agent_radius; p.goal_thr = c.goal_threshold; p.min_spawn = c.min_spawn_dist;
   p.thr_agent = c.spawn_thresh_agent; p.thr_goal = c.spawn_thresh_goal;
   // the obstacle loops run MAXS slots branch-free: the smallest bound that covers num_static
-  void (*fn)(BParams) = c.num_static <= 4    ? board_kernel<4>
-                        : c.num_static <= 6  ? board_kernel<6>
-                        : c.num_static <= 8  ? board_kernel<8>
-                        : c.num_static <= 12 ? board_kernel<12>
-                        : c.num_static <= 16 ? board_kernel<16>
-                                             : board_kernel<32>;
+  void (*fn)(BParams) = nullptr;
+  if (mode == 3)
+    fn = c.num_static <= 4    ? board_kernel<4, true>
+         : c.num_static <= 6  ? board_kernel<6, true>
+         : c.num_static <= 8  ? board_kernel<8, true>
+         : c.num_static <= 12 ? board_kernel<12, true>
+         : c.num_static <= 16 ? board_kernel<16, true>
+                              : board_kernel<32, true>;
+  else
+    fn = c.num_static <= 4    ? board_kernel<4>
+         : c.num_static <= 6  ? board_kernel<6>
+         : c.num_static <= 8  ? board_kernel<8>
+         : c.num_static <= 12 ? board_kernel<12>
+         : c.num_static <= 16 ? board_kernel<16>
+                              : board_kernel<32>;
   hipLaunchKernelGGL(fn, dim3((unsigned)((c.num_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p);
   e = hipGetLastError();
   if (e != hipSuccess) return bhip(b, e);
@@ -495,6 +519,11 @@ int be_board_reset(be_board* b, const be_board_state* st, const uint8_t* mask, c
 int be_board_step(be_board* b, const be_board_state* st, const uint8_t* actions, const double* deltas,
                   const be_board_out* out, void* stream) {
   return board_launch(b, st, out, 0, actions, deltas, nullptr, nullptr, 0, stream);
+}
+
+int be_board_rollout(be_board* b, const be_board_state* st, const uint8_t* actions, const double* deltas,
+                     int32_t steps, const be_board_out* out, void* stream) {
+  return board_launch(b, st, out, 3, actions, deltas, nullptr, nullptr, 0, stream, steps);
 }
 
 int be_board_observe(be_board* b, const be_board_state* st, const be_board_out* out, void* stream) {

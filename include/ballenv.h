@@ -310,6 +310,13 @@ int be_board_reset(be_board* b, const be_board_state* st, const uint8_t* mask, c
 int be_board_step(be_board* b, const be_board_state* st, const uint8_t* actions, const double* deltas,
                   const be_board_out* out, void* stream);
 /* featureExtractor of the current state (no state change). */
+/* `steps` consecutive be_board_step calls in one launch, each env's state in registers:
+ * actions (steps, N) u8 or deltas (steps, N, 2) f64; out->reward / done / truncated
+ * (steps, N) and out->features (steps, N, 20) or NULL.  Philox resets only (no tape).
+ * Bit-identical to `steps` be_board_step calls (the caller's per-step loop over
+ * createBoard.step, ballenv_pygame.py:650-675, for every env).                      */
+int be_board_rollout(be_board* b, const be_board_state* st, const uint8_t* actions, const double* deltas,
+                     int32_t steps, const be_board_out* out, void* stream);
 int be_board_observe(be_board* b, const be_board_state* st, const be_board_out* out, void* stream);
 int be_board_status(be_board* b, int32_t* status_out, void* stream);
 

@@ -148,3 +148,36 @@ def test_gpu_board_autoreset_and_observe(gpu):
     assert torch.equal(b.observe(), f1)      # observe() == the features step() wrote
     b.status()
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_deltas", [False, True])
+def test_gpu_board_rollout_matches_steps(gpu, use_deltas):
+    """be_board_rollout == that many be_board_step calls, bit for bit (features, reward, done,
+    truncated, state), through autoresets (wave-cooperative Philox) and a partial last block."""
+    N, K = 5000, 45
+    a, b = (make_board(gpu, N, 6, seed=4, autoreset=True, time_limit=20) for _ in range(2))
+    a.reset()
+    b.reset()
+    g = torch.Generator(device="cpu").manual_seed(2)
+    if use_deltas:
+        mv = (torch.randn(K, N, 2, generator=g, dtype=torch.float64) * 3).to(gpu)
+    else:
+        mv = torch.randint(0, 4, (K, N), generator=g, dtype=torch.uint8).to(gpu)
+    ref = {"f": [], "r": [], "d": [], "t": []}
+    for t in range(K):
+        f, r, d, info = a.step(deltas=mv[t]) if use_deltas else a.step(mv[t])
+        ref["f"].append(f.clone()); ref["r"].append(r.clone()); ref["d"].append(d.clone())
+        ref["t"].append(info["truncated"].clone())
+    f, r, d, info = b.rollout(deltas=mv) if use_deltas else b.rollout(mv)
+    assert torch.equal(f, torch.stack(ref["f"]))
+    assert torch.equal(r, torch.stack(ref["r"]))
+    assert torch.equal(d, torch.stack(ref["d"]))
+    assert torch.equal(info["truncated"], torch.stack(ref["t"]))
+    assert bool(d.any())
+    for k in a.STATE_KEYS:
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    a.status()
+    b.status()
+    a.close()
+    b.close()
