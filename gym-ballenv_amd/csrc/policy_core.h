@@ -41,17 +41,11 @@ __host__ __device__ constexpr PolLayout pol_layout(int HT, int KS, int NO) {
   return L;
 }
 
-// x summed over lanes l, l^16, l^32, l^48 (the 4 lane groups), on the VALU
-__device__ __forceinline__ float sum_groups(float x) {
-  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
 
-// sum_groups of four values at once: lane group (row) r gets the full sum of value r, each
-// added in sum_groups' order ((g0 + g1) + (g2 + g3)) -- two permlane16 swaps pair the values'
-// rows, one permlane32 swap finishes all four (6 instructions instead of 16).
+// Sum over the 4 lane groups (lanes l, l^16, l^32, l^48) of four values at once: lane group
+// (row) r gets the full sum of value r, added as ((g0 + g1) + (g2 + g3)) -- two permlane16
+// swaps pair the values' rows, one permlane32 swap finishes all four (6 VALU instructions
+// where one value at a time takes 16).
 __device__ __forceinline__ float sum_groups4(float x0, float x1, float x2, float x3) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
   const float c = __uint_as_float(a[0]) + __uint_as_float(a[1]);   // rows: x0 01, x1 01, x0 23, x1 23
@@ -72,9 +66,6 @@ __device__ __forceinline__ void sum_outputs(const float (&part)[NO], float (&out
   }
 }
 
-#ifndef BE_POL_UNROLL
-#define BE_POL_UNROLL 13
-#endif
 
 // OR of x over lanes l, l^16, l^32, l^48
 __device__ __forceinline__ uint32_t or_groups(uint32_t x) {

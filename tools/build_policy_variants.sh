@@ -1,6 +1,6 @@
 #!/bin/bash
 # Diagnostics builds of libballenv.so with extra compile flags -> tools/diag/libballenv_<NAME>.so
-# each argument: NAME:FLAGS, e.g. u1:-DBE_POL_UNROLL=1
+# each argument: NAME:FLAGS, e.g. nofma:-DSOME_DIAG_FLAG=1
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/diag

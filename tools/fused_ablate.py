@@ -6,7 +6,7 @@ Policy(10)) under ablation bits -- a diagnostics build reads them (BE_DIAG_SKIP)
 dbg bits (csrc/ballenv.hip): 2048 every env on the empty-window table (no MFMA tiles),
 4096 no select_action tail (a fixed action hash), 8192 no block barriers (with 2048 only),
 0x20000 tile_forward without MFMA, 0x40000 tile_forward without head FMAs.
-``--build [unroll ...]`` also builds tools/diag/skip_u<n>/ with BE_POL_UNROLL=n.
+``--build [name:flag ...]`` also builds tools/diag/skip_<name>/ with extra compile flags.
 Also times the tape-driven be_rollout of the same envs for reference.  Outputs under
 ablation are wrong by design; only the time is meaningful.
 """
@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 def build(unrolls):
     from gym_ballenv_amd.build import build_library
     for u in [None, *unrolls]:
-        sub, flags = ("skip", ["-DBE_DIAG_SKIP"]) if u is None else (f"skip_u{u}", ["-DBE_DIAG_SKIP", f"-DBE_POL_UNROLL={u}"])
+        sub, flags = ("skip", ["-DBE_DIAG_SKIP"]) if u is None else (f"skip_{u.split(':')[0]}", ["-DBE_DIAG_SKIP", u.split(':', 1)[1]])
         out = os.path.join(ROOT, "tools", "diag", sub, "libballenv.so")
         os.makedirs(os.path.dirname(out), exist_ok=True)
         build_library(extra_flags=flags, out=out)
@@ -86,6 +86,6 @@ def main():
 
 if __name__ == "__main__":
     if "--build" in sys.argv:
-        build([int(x) for x in sys.argv[2:]])
+        build(sys.argv[2:])
     else:
         main()
