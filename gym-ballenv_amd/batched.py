@@ -187,10 +187,12 @@ class BatchedBallEnv:
         ``truncated`` / ``final_return`` / ``final_len`` (K, N) -- exactly what K calls of
         :meth:`step` return, stacked (the reference's per-step loop of
         examples/ball_cnn_ac3.py:573-600, for every env).  The state advances by K steps.
-        u8 obs only; the buffers are reused by the next rollout of the same K.
+        With ``terminal_obs=True`` info also holds ``terminal_obs`` (K, N, F), written for
+        the rows of envs that reset on that step.  u8 obs only; the buffers are reused by the
+        next rollout of the same K.
         """
-        if self._want_f32 or self._want_terminal:
-            raise ValueError("rollout() returns u8 obs only (build the env without obs_f32 / terminal_obs)")
+        if self._want_f32:
+            raise ValueError("rollout() returns u8 obs only (build the env without obs_f32)")
         a = actions if actions.dtype == torch.uint8 else actions.to(torch.uint8)
         if a.device != self.device:
             a = a.to(self.device)
@@ -202,15 +204,19 @@ class BatchedBallEnv:
         if buf is None or buf[0].shape[0] != K:
             z = lambda *shape, dt: torch.zeros(*shape, dtype=dt, device=self.device)  # noqa: E731
             buf = (z(K, N, F, dt=torch.uint8), z(K, N, dt=torch.float64), z(K, N, dt=torch.bool),
-                   z(K, N, dt=torch.bool), z(K, N, dt=torch.float64), z(K, N, dt=torch.int32))
+                   z(K, N, dt=torch.bool), z(K, N, dt=torch.float64), z(K, N, dt=torch.int32),
+                   z(K, N, F, dt=torch.uint8) if self._want_terminal else None)
             self._ro_buf = buf
-        obs, reward, done, trunc, fret, flen = buf
-        out = _abi.BeOut(obs.data_ptr(), None, reward.data_ptr(), done.data_ptr(), trunc.data_ptr(), None,
+        obs, reward, done, trunc, fret, flen, term = buf
+        out = _abi.BeOut(obs.data_ptr(), None, reward.data_ptr(), done.data_ptr(), trunc.data_ptr(), _ptr(term),
                          fret.data_ptr(), flen.data_ptr(), self.stats_buf.data_ptr() if self._track_stats else None)
         _abi.check(self._lib.be_rollout(self._ctx, C.byref(self._st), a.data_ptr(), int(K), C.byref(out),
                                         self._stream()), self._ctx)
         self._keep = (a,)
-        return obs, reward, done, {"truncated": trunc, "final_return": fret, "final_len": flen}
+        info = {"truncated": trunc, "final_return": fret, "final_len": flen}
+        if term is not None:
+            info["terminal_obs"] = term
+        return obs, reward, done, info
 
     def observe(self) -> torch.Tensor:
         """prep_state4 of the current state (no state change)."""

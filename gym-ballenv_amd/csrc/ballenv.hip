@@ -1778,6 +1778,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     int gxr = gx, gyr = gy;
     const unsigned long long m = __ballot(valid && done && p.autoreset);
     if (m) {
+      if (p.terminal_obs && valid && done) {   // obs of the terminal state, rows of reset envs (as be_step)
+        const Win g(p, ax, ay);
+        uint32_t rows[KR], flat[Geo<WT>::NW];
+        raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, t.hw);
+        flatten<WT>(rows, flat);
+        write_row_global<WT>(p.terminal_obs + (so_n + i) * F, flat, quadrant(ax, ay, gx, gy));
+      }
       int32_t* ost = &s_ost[w][0];
       auto osink = [&](int sl, int k, int, int32_t o) { ost[sl * G + k] = o; };
       auto esink = [&](int own, int32_t ag, int32_t go, int32_t a0) {
@@ -2257,8 +2264,7 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
   if (!actions || steps < 0) return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs actions and steps >= 0");
   if (!out || !out->obs || !out->reward || !out->done)
     return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs out->obs, out->reward and out->done");
-  if (out->obs_f32 || out->terminal_obs)
-    return fail(ctx, BE_E_INVALID, "%s", "be_rollout writes u8 obs only (obs_f32 / terminal_obs must be NULL)");
+  if (out->obs_f32) return fail(ctx, BE_E_INVALID, "%s", "be_rollout writes u8 obs only (obs_f32 must be NULL)");
   const int64_t N = ctx->cfg.num_envs, F = 4 + (int64_t)ctx->cfg.window * ctx->cfg.window;
   if (((uintptr_t)out->obs & 15) || (N * F) % 16)
     return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs a 16-byte aligned obs and num_envs * (4+W*W) % 16 == 0");
@@ -2282,6 +2288,7 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
     o.reward = out->reward + s * N;
     o.done = out->done + s * N;
     if (o.truncated) o.truncated = out->truncated + s * N;
+    if (o.terminal_obs) o.terminal_obs = out->terminal_obs + s * N * F;
     if (o.final_return) o.final_return = out->final_return + s * N;
     if (o.final_len) o.final_len = out->final_len + s * N;
     if (int rc = be_step(ctx, st, actions + s * N, nullptr, nullptr, &o, stream)) return rc;

@@ -175,8 +175,9 @@ int be_step(be_ctx* ctx, const be_state* st, const uint8_t* actions, const int16
 /* `steps` consecutive be_step calls in one launch (a fused rollout), for an action tape.
  * actions: (steps, N) u8 indices into cfg.actions.  Outputs are per step: out->obs
  * (steps, N, 4+W*W) u8, out->reward (steps, N) f64, out->done / truncated (steps, N) u8,
- * out->final_return / final_len (steps, N) (done rows only); out->stats accumulates as for
- * be_step.  out->obs_f32 and out->terminal_obs must be NULL; N*(4+W*W) must be a multiple of 16.
+ * out->final_return / final_len (steps, N) and out->terminal_obs (steps, N, 4+W*W) (rows of
+ * reset envs only), or NULL; out->stats accumulates as for be_step.  out->obs_f32 must be
+ * NULL; N*(4+W*W) must be a multiple of 16.
  * Results are bit-identical to `steps` be_step calls with actions + s*N (same state, same
  * Philox draws).  The reference has no batched counterpart: it is the caller's loop
  *   for t: state, reward, done, _ = env.step(move_list[a_t]); prep_state4(state)

@@ -17,9 +17,9 @@ from test_gpu_parity import KEYS, make_env, np_state
 pytestmark = pytest.mark.gpu
 
 
-def _run_pair(cfg_py, N, W, K, chunks, seed=7):
+def _run_pair(cfg_py, N, W, K, chunks, seed=7, terminal=False):
     """Env A: K be_step calls.  Env B: be_rollout over `chunks` (step counts summing to K)."""
-    a, b = make_env(cfg_py, N, W, "cuda:0", seed=seed), make_env(cfg_py, N, W, "cuda:0", seed=seed)
+    a, b = (make_env(cfg_py, N, W, "cuda:0", seed=seed, terminal_obs=terminal) for _ in range(2))
     acts = a.sample_actions(K, seed=seed + 1)
     a.reset()
     b.reset()
@@ -32,6 +32,8 @@ def _run_pair(cfg_py, N, W, K, chunks, seed=7):
         ref["truncated"][t] = info["truncated"].cpu().numpy()
         ref["final_return"][t] = info["final_return"].cpu().numpy()
         ref["final_len"][t] = info["final_len"].cpu().numpy()
+        if terminal:
+            ref.setdefault("terminal_obs", np.zeros((K, N, F), np.uint8))[t] = info["terminal_obs"].cpu().numpy()
     t0 = 0
     for k in chunks:
         obs, r, d, info = b.rollout(acts[t0:t0 + k])
@@ -43,6 +45,8 @@ def _run_pair(cfg_py, N, W, K, chunks, seed=7):
         dm = ref["done"][sl]   # final_* are written for done rows only
         np.testing.assert_array_equal(info["final_return"].cpu().numpy()[dm], ref["final_return"][sl][dm])
         np.testing.assert_array_equal(info["final_len"].cpu().numpy()[dm], ref["final_len"][sl][dm])
+        if terminal:   # rows of envs that reset on that step
+            np.testing.assert_array_equal(info["terminal_obs"].cpu().numpy()[dm], ref["terminal_obs"][sl][dm])
         t0 += k
     assert t0 == K
     sa, sb = np_state(a), np_state(b)
@@ -67,16 +71,17 @@ def test_rollout_matches_steps_default(gpu, W, N):
 
 @pytest.mark.parametrize("W", [10, 5])
 def test_rollout_mass_truncation(gpu, W):
-    """time_limit 20: every env of every wave resets on the same steps (multi-env reset passes)."""
+    """time_limit 20: every env of every wave resets on the same steps (multi-env reset passes);
+    terminal_obs rows of the reset envs equal be_step's."""
     from gym_ballenv_amd.config import EnvConfig
-    n_done = _run_pair(EnvConfig(time_limit=20), 20000, W, 45, (45,))
+    n_done = _run_pair(EnvConfig(time_limit=20), 20000, W, 45, (45,), terminal=True)
     assert n_done >= 2 * 20000
 
 
 def test_rollout_generic_config(gpu):
     """A config outside the fixed shape (7 static + 3 dynamic, W=7): be_rollout loops be_step."""
     from gym_ballenv_amd.config import EnvConfig
-    _run_pair(EnvConfig(num_static=7, num_dynamic=3, time_limit=30), 2048, 7, 40, (40,))
+    _run_pair(EnvConfig(num_static=7, num_dynamic=3, time_limit=30), 2048, 7, 40, (40,), terminal=True)
 
 
 def test_rollout_errors(gpu):
