@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--window", type=int, default=10)
     p.add_argument("--mode", choices=["graph", "eager"], default="graph")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--cpu-procs", type=int, default=8)
+    p.add_argument("--cpu-procs", type=int, default=0, help="0 = one per usable host core")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph-chunk", type=int, default=250, help="steps per captured graph")
     p.add_argument("--policy-steps", type=int, default=1000,
@@ -66,24 +66,53 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(window, seconds, procs):
-    """Reference algorithm (scalar Python port) on the host cores; no GPU touched."""
+def host_cores():
+    """CPUs this process may actually use: the affinity mask, capped by a cgroup-v2 CPU quota
+    (on a shared GPU box os.cpu_count() and the affinity mask show the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_baseline(window, seconds, procs=None):
+    """Reference algorithm (scalar Python port of BallEnv.step + prep_state4, oracle/py_ballenv.py)
+    on the host cores, SURVEY.md 8(d): single env per process, one process per usable core, at
+    W=5 and W=10 (per-core and aggregate rates), plus BASELINE config 1 (one single-env W=5
+    100-step rollout).  No GPU is touched.  `value` is the headline window's aggregate."""
     from oracle import py_ballenv
     import multiprocessing as mp
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    procs = max(1, min(procs, avail))
+    cores = host_cores() if not procs else min(procs, host_cores())
     ctx = mp.get_context("fork")
-    with ctx.Pool(procs) as pool:
-        res = pool.map(py_ballenv._worker, [(window, seconds, 1000 + i) for i in range(procs)])
-    steps = sum(s for s, _ in res)
-    el = max(t for _, t in res)
-    return {"value": steps / el, "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} procs x {seconds:.0f} s: single-env BallEnv.step + prep_state4 (W={window}), "
-                      f"13 static + 5 dynamic obstacles, uniform random 9-way actions, reset on done/1000 steps; "
-                      f"{steps} env-steps in {el:.1f} s (oracle/py_ballenv.py, pure Python)"}
+    by_w = {}
+    per_w = seconds / 2.0
+    with ctx.Pool(cores) as pool:
+        for w in (5, 10):
+            res = pool.map(py_ballenv._worker, [(w, per_w, 1000 + i) for i in range(cores)])
+            steps = sum(s for s, _ in res)
+            el = max(t for _, t in res)
+            rates = [s / t for s, t in res]
+            by_w[w] = {"aggregate": steps / el, "per_core_mean": sum(rates) / len(rates),
+                       "per_core_min": min(rates), "per_core_max": max(rates), "env_steps": steps,
+                       "seconds": el}
+    n1, t1 = py_ballenv.run_rollout(5, 100, seed=7)
+    hw = by_w.get(window, by_w[10])
+    return {"value": hw["aggregate"], "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "per_core": hw["per_core_mean"],
+            "by_window": {f"W={w}": v for w, v in by_w.items()},
+            "config1": {"what": "BASELINE config 1: single env, W=5, one 100-step random-action rollout, 1 core",
+                        "seconds": t1, "env_steps_per_s": n1 / t1},
+            "sample": f"{cores} procs (one per usable core: affinity mask, cgroup quota) x {per_w:.0f} s at W=5 "
+                      f"and at W=10: single-env BallEnv.step + prep_state4, 13 static + 5 dynamic obstacles, "
+                      f"uniform random 9-way actions, reset on done/1000 steps (oracle/py_ballenv.py, pure "
+                      f"Python); value = W={window if window in by_w else 10} aggregate"}
 
 
 def timed_graph_steps(graphs, steps, dev, stream, world):
@@ -151,10 +180,7 @@ def policy_leg(args, gb, dev, rank, world, stream):
             hp._lib.be_policy_act(hp._h, C.byref(env._st), env.obs.data_ptr(), C.byref(ro._act_outs[0]), 7, sp)
     g.replay()
     _, pms = timed_graph_steps([g], T, dev, stream, world)
-    H = pol.hidden_layer
-    flops = 2.0 * N * (4 + W * W) * H * 3           # int8 MFMA ops issued for fc1 (3 digit passes)
-    res.update({"policy_kernel_us": pms * 1e3, "packed_weight_bytes": hp.packed_bytes,
-                "fc1_int8_tops": flops / (pms * 1e-3) / 1e12})
+    res.update({"policy_kernel_us": pms * 1e3, "packed_weight_bytes": hp.packed_bytes})
     episodes = env.episode_stats()
     res["episodes"] = {k: episodes[k] for k in ("episodes", "mean_return", "mean_length")}
     del g
@@ -164,6 +190,7 @@ def policy_leg(args, gb, dev, rank, world, stream):
     env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
     env.reset()
     ro = gb.Rollout(env, pol, horizon=T, backend="fused", seed=0x5E1EC7, chunk=args.rollout_chunk)
+    ro_chunk, img_bytes = ro.chunk, ro.hp.packed_bytes
     ro.run()                                         # warm-up horizon
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -207,7 +234,52 @@ def policy_leg(args, gb, dev, rank, world, stream):
         ro.close()
         env.close()
     fused["two_launch"] = res
+    fused["roofline"] = policy_roofline(args, gb, dev, rank, pol, fused["kernel_us_per_step"], ro_chunk, img_bytes)
     return fused
+
+
+def policy_roofline(args, gb, dev, rank, pol, us_per_step, chunk, img):
+    """Roofline of the fused config-5 kernel on what it actually issues.
+
+    fc1 runs on the int8 matrix cores only for envs whose window has a lit cell: each
+    workgroup (256 envs) packs those into 16-env tiles, and each tile costs HT x KS x 3
+    v_mfma_i32_16x16x64_i8 (hidden-row tiles x K-steps x 3 digit planes, csrc/policy_core.h).
+    The envs with an empty window read their logits from a 4-entry table (no MFMA).  The tile
+    count per step is measured on a recorded rollout of the same env batch and policy (the
+    policy input obs of every step), so `achieved` counts MFMA ops issued, not 2*N*F*H."""
+    import torch
+    from gym_ballenv_amd.rollout import Rollout
+    N, W, T = args.envs, args.window, 100
+    env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
+    env.reset()
+    ro = Rollout(env, pol, horizon=T, backend="fused", record_obs=True, seed=0x5E1EC7, chunk=T)
+    ro.run()
+    lit = (ro.obs[:T, :, 4:] != 0).any(-1).to(torch.int32)             # (T, N): policy input has a lit cell
+    nb = (N + 255) // 256
+    per_block = torch.nn.functional.pad(lit, (0, nb * 256 - N)).view(T, nb, 256).sum(-1)
+    tiles = (per_block + 15) // 16
+    tiles_per_step = float(tiles.sum()) / T
+    lit_frac = float(lit.sum()) / (T * N)
+    ro.close()
+    env.close()
+    F = 4 + W * W
+    HT, KS = -(-pol.hidden_layer // 16), -(-F // 64)
+    mfma_per_tile = HT * KS * 3
+    ops_step = tiles_per_step * mfma_per_tile * 2 * 16 * 16 * 64
+    achieved = ops_step / (us_per_step * 1e-6) / 1e12
+    peak = 5000.0      # dense int8 MFMA TOP/s (2x the ~2.5 PFLOP/s dense bf16 rate, MI355X_MICROARCH.md)
+    # HBM bytes per env-step: action 1 + log_prob 4 + value 4 + reward 8 + done 1 per step, the engine
+    # state read+write (161 B at the defaults) and the packed policy image (per workgroup) once per launch
+    B_state = gb.step_bytes(gb.EnvConfig(), W) - (1 + 8 + 1 + 4 + W * W)
+    B = 18 + B_state / chunk + (img * nb) / (chunk * N)
+    return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TOP/s", "frac": achieved / peak,
+            "traffic": None, "tiles_per_step": tiles_per_step, "lit_env_frac": lit_frac,
+            "mfma_per_tile": mfma_per_tile, "int8_ops_issued_per_step": ops_step,
+            "hbm_bytes_per_env_step": B, "hbm_GBs": B * N / (us_per_step * 1e-6) / 1e9,
+            "hbm_frac": B * N / (us_per_step * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "limiter": "neither roofline: issue/latency-bound at 4 waves per SIMD (the env physics, the per-step "
+                       "block barrier + list + draw, then the dense tiles of the few lit envs); PMC counters in "
+                       "profiles/r02_pmc_policy_rollout.json"}
 
 
 def rollout_leg(args, gb, dev, rank, world, stream):
@@ -400,6 +472,11 @@ def main():
                     launch(t, cs)
             graphs.append(g)
         torch.cuda.synchronize(dev)
+        # one untimed replay of every captured graph (its first launch uploads it and pays the
+        # clock ramp); it steps the envs, like the eager warm-up above, on actions rows 0..K-1
+        for g in graphs:
+            g.replay()
+        torch.cuda.synchronize(dev)
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -418,12 +495,16 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    n_devices = 1
     if world > 1:
         el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
         per_rank = gb.gather_stats(env.stats_record())            # RCCL all_gather of episode returns
         ep = gb.combine_stats(per_rank)
+        devs = [None] * world                                      # distinct GPUs, not ranks (gloo rehearsal)
+        dist.all_gather_object(devs, (os.uname().nodename, str(torch.cuda.get_device_properties(dev).uuid)))
+        n_devices = len(set(devs))
     else:
         ep = env.episode_stats()
     env.status()
@@ -438,12 +519,14 @@ def main():
 
     # HBM-side bytes per launch from the committed PMC passes (tools/pmc_bench.sh):
     # 2 x FETCH_SIZE (gfx950 reports half of wide reads) + WRITE_SIZE, same kernel / envs / W
+    # (committed profile, used only when it was taken on the kernel this run launched, same envs/W)
+    kname = env.kernel_name("step")
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     if os.path.exists(pmc):
         d = json.load(open(pmc))
-        if d.get("envs") == N and d.get("window") == W:
-            traffic, traffic_src = d.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT)
+        if d.get("envs") == N and d.get("window") == W and f"::{kname}(" in (d.get("kernel") or ""):
+            traffic, traffic_src = d.get("hbm_bytes_per_launch"), "committed profile " + os.path.relpath(pmc, ROOT)
 
     pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
     board_res = board_leg(args, gb, dev, rank, world, stream) if args.board_steps > 0 else None
@@ -452,9 +535,9 @@ def main():
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), batch=65536 envs, window=10; achieved HBM GB/s",
-            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": WU,
+            "value": value, "unit": "env-steps/s", "n_gpus": n_devices, "ranks": world, "steps": K, "warmup": WU,
             "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int32+f64", "data": "synthetic",
+            "vs_baseline": None, "dtype": "int16x2+f64", "data": "synthetic",
             "config": {"workload": f"BallEnv step + prep_state4 window, random actions, {N} envs/GPU, W={W}, "
                                    "13 static + 5 dynamic obstacles, TimeLimit 1000, autoreset",
                        "envs_per_gpu": N, "global_envs": N * world, "window": W,
@@ -465,7 +548,7 @@ def main():
                          "bytes_per_env_step": B, "bytes_source": "SURVEY.md 8(d): 82+8*Ns+20*Nd+4+W^2",
                          "engine_bytes_per_env_step": B_eng, "engine_achieved": achieved_eng,
                          "engine_frac": achieved_eng / HBM_PEAK_GBS, "kernel_us_mean": kern_ms * 1e3,
-                         "kernel": f"be_kernel<{W}, 0> (MODE_STEP)", "traffic_source": traffic_src},
+                         "kernel": kname, "traffic_source": traffic_src},
             "cpu_baseline": base,
             "episodes": ep,
             "policy_rollout": pol_res,

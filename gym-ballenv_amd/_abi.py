@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_STATIC, MAX_DYNAMIC, MAX_GOALS, MAX_ACTIONS, MAX_WINDOW = 64, 32, 16, 16, 64
 
 BE_OK, BE_E_INVALID, BE_E_HIP, BE_E_NOMEM, BE_E_DEVICE = 0, -1, -2, -3, -4
@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("BALLENV_LIB") or os.path.join(os.path.dirname(os.path
 
 # Names declared in include/ballenv.h (checked by tests/test_abi.py).
 EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_bytes", "be_stats_slots",
-           "be_last_error",
+           "be_last_error", "be_kernel_name",
            "be_create", "be_destroy", "be_reset", "be_step", "be_rollout", "be_observe", "be_sample_actions",
            "be_status", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
            "be_policy_rollout", "be_policy_bytes", "be_observe_blocks",
@@ -117,6 +117,7 @@ def lib() -> C.CDLL:
         "be_step_bytes": (i64, [P(BeConfig)]),
         "be_stats_slots": (i64, [P(BeConfig)]),
         "be_last_error": (C.c_char_p, [vp]),
+        "be_kernel_name": (C.c_char_p, [vp, i32]),
         "be_create": (C.c_int, [P(BeConfig), i32, P(vp)]),
         "be_destroy": (C.c_int, [vp]),
         "be_reset": (C.c_int, [vp, P(BeState), vp, vp, i32, P(BeOut), vp]),

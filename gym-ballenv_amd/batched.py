@@ -245,6 +245,14 @@ class BatchedBallEnv:
                                                self._stream()), self._ctx)
         return out
 
+    def kernel_name(self, entry: str = "step") -> Optional[str]:
+        """Name of the kernel an entry point launches for this env (rocprofv3's kernel name
+        without namespace / arguments): entry in step (caller actions), step_sampled,
+        rollout (None: be_rollout loops be_step), reset, observe."""
+        ids = {"step": 0, "step_sampled": 1, "rollout": 2, "reset": 3, "observe": 4}
+        r = self._lib.be_kernel_name(self._ctx, ids[entry])
+        return r.decode() if r else None
+
     # ------------------------------------------------------------------ bookkeeping
     def status(self) -> int:
         """Synchronise and read (then clear) the device status word; raises on error bits."""

@@ -1898,7 +1898,7 @@ KFn kernel_for(int mode) {
                            : (mode == MODE_RESET ? be_kernel<WT, MODE_RESET> : be_kernel<WT, MODE_OBSERVE>);
 }
 
-struct Launch { KFn fn; int epb; int lds; };
+struct Launch { KFn fn; int epb; int lds; char name[48]; };
 
 // Fixed-shape step kernels for the reference's default obstacle counts (ball_cnn_ac3.py:40-41).
 constexpr int FIX_NS = 13, FIX_ND = 5;
@@ -1921,6 +1921,10 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false) {
 #undef BE_CASE
     default: L.fn = kernel_for<0>(mode); L.epb = envs_per_block(0); staged = false; break;
   }
+  if (L.fn) {
+    if (W == -1) snprintf(L.name, sizeof L.name, "be_kernel<%d, %d, %d, %d>", c.window, mode, FIX_NS, FIX_ND);
+    else snprintf(L.name, sizeof L.name, "be_kernel<%d, %d, 0, 0>", staged ? W : 0, mode);
+  }
   const int near_bytes = (nobs + 1) * BLOCK_THREADS * 4;   // +1: predicated pushes write one slot ahead
   const int stage_bytes = staged ? L.epb * F : 0;
   L.lds = (near_bytes + stage_bytes + 15) & ~15;
@@ -1936,6 +1940,7 @@ Launch pick_rollout(const be_config& c, bool fixed_ok) {
   if (fixed && c.window == 10) L.fn = rollout_kernel<10, FIX_NS, FIX_ND>;
   else if (fixed && c.window == 5) L.fn = rollout_kernel<5, FIX_NS, FIX_ND>;
   L.lds = ((FIX_NS + FIX_ND + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * (4 + c.window * c.window) + 15) & ~15;
+  if (L.fn) snprintf(L.name, sizeof L.name, "rollout_kernel<%d, %d, %d, 0, 1, 10>", c.window, FIX_NS, FIX_ND);
   return L;
 }
 
@@ -2094,6 +2099,24 @@ int64_t be_step_bytes(const be_config* c) {
 }
 
 const char* be_last_error(const be_ctx* ctx) { return ctx ? ctx->err : g_err; }
+
+const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
+  static thread_local char name[48];
+  if (!ctx) return nullptr;
+  const bool fixed_ok = !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals;
+  Launch L{nullptr, 0, 0, {0}};
+  switch (entry) {
+    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok); break;
+    case BE_ENTRY_STEP_SAMPLED: L = pick_kernel(ctx->cfg, MODE_STEP, false); break;
+    case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok); break;
+    case BE_ENTRY_RESET: L = pick_kernel(ctx->cfg, MODE_RESET, false); break;
+    case BE_ENTRY_OBSERVE: L = pick_kernel(ctx->cfg, MODE_OBSERVE, false); break;
+    default: return nullptr;
+  }
+  if (!L.fn) return nullptr;
+  memcpy(name, L.name, sizeof name);
+  return name;
+}
 
 int64_t be_stats_slots(const be_config* c) {
   if (!c || c->num_envs < 1 || c->window < 1) return 0;

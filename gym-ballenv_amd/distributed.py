@@ -30,9 +30,12 @@ def gather_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     if not (dist.is_available() and dist.is_initialized()):
         return stats.reshape(1, -1).clone()
     world = dist.get_world_size(group)
-    out = [torch.empty_like(stats) for _ in range(world)]
-    dist.all_gather(out, stats.contiguous(), group=group)
-    return torch.stack(out)
+    src = stats.contiguous()
+    if src.is_cuda and dist.get_backend(group) == "gloo":   # gloo rehearsal: gather through the host
+        src = src.cpu()
+    out = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(out, src, group=group)
+    return torch.stack(out).to(stats.device)
 
 
 def combine_stats(per_rank: torch.Tensor) -> dict:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BE_ABI_VERSION 4
+#define BE_ABI_VERSION 5
 
 #define BE_MAX_STATIC   64
 #define BE_MAX_DYNAMIC  32
@@ -150,6 +150,15 @@ int64_t be_step_bytes(const be_config* cfg);
 /* Number of 8-double slots the be_out.stats buffer must hold for this config. */
 int64_t be_stats_slots(const be_config* cfg);
 const char* be_last_error(const be_ctx* ctx);
+
+/* Which kernel an entry point launches for this context (for profiles and bench lines: the
+ * name matches rocprofv3's kernel name without the namespace/argument list), or NULL for a
+ * bad ctx / entry.  No GPU work.  Diagnostics only; the reference has no counterpart. */
+enum { BE_ENTRY_STEP_ACTIONS = 0,   /* be_step with caller action indices           */
+       BE_ENTRY_STEP_SAMPLED = 1,   /* be_step with in-kernel sampled actions       */
+       BE_ENTRY_ROLLOUT = 2,        /* be_rollout (NULL name: it loops be_step)     */
+       BE_ENTRY_RESET = 3, BE_ENTRY_OBSERVE = 4 };
+const char* be_kernel_name(const be_ctx* ctx, int32_t entry);
 
 /* ---- device functions ---- */
 int be_create(const be_config* cfg, int32_t device, be_ctx** out);

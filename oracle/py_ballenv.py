@@ -257,3 +257,21 @@ def run_baseline_parallel(window: int, seconds: float, procs: int):
     total = sum(s for s, _ in res)
     el = max(t for _, t in res)
     return total, el, [s / t for s, t in res]
+
+
+def run_rollout(window: int, steps: int, seed: int = 0, time_limit: int = 1000):
+    """BASELINE config 1: ONE single-env rollout of exactly `steps` random-action steps
+    (step + prep_state4, reset on done).  Returns (steps, elapsed_seconds)."""
+    np.random.seed(seed)
+    arng = np.random.RandomState(seed + 1)
+    env = PyBallEnv()
+    t0 = time.perf_counter()
+    state = env.reset()
+    env.prep_state4(state, window)
+    for _ in range(steps):
+        state, reward, done = env.step(MOVE_LIST[arng.randint(9)])
+        env.prep_state4(state, window)
+        if done or env.elapsed >= time_limit:
+            state = env.reset()
+            env.prep_state4(state, window)
+    return steps, time.perf_counter() - t0

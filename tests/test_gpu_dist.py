@@ -1,0 +1,88 @@
+"""Multi-rank engine rehearsal on one GPU (BASELINE config 4's code path).
+
+A fresh child `python -m torch.distributed.run --nproc-per-node 2` (gloo; both ranks on
+cuda:0; started as a new process, never an exec) runs tests/dist_engine_worker.py: each rank
+steps its shard() of 8192 envs for 120 default-config steps and all_gathers its stats record.
+This process then runs the whole batch on one rank and checks, bit for bit, that the ranks'
+per-env rewards / dones / obs, their final states, their per-wave stats slots and the gathered
+records equal the matching rows of the one-rank run (Philox streams are keyed by global env id).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_engine_matches_one_rank(gpu, tmp_path):
+    import gym_ballenv_amd as gb
+    E, T, W, seed, world = 8192, 120, 10, 0xD157, 2
+    env_vars = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(HERE, "dist_engine_worker.py"), "--out", str(tmp_path), "--envs", str(E),
+           "--steps", str(T), "--window", str(W), "--seed", str(seed)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env_vars, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    ranks = [dict(np.load(tmp_path / f"rank{i}.npz")) for i in range(world)]
+
+    # the same global batch on one rank
+    env = gb.BatchedBallEnv(E, W, gb.EnvConfig(), device=gpu, seed=seed)
+    env.reset()
+    acts = env.sample_actions(T, seed=seed)
+    rew = np.empty((T, E))
+    done = np.empty((T, E), bool)
+    bits = np.empty((T, E, (env.obs_dim + 7) // 8), np.uint8)
+    for t in range(T):
+        obs, rw, d, _ = env.step(acts[t])
+        rew[t], done[t], bits[t] = rw.cpu().numpy(), d.cpu().numpy(), np.packbits(obs.cpu().numpy(), axis=1)
+    env.status()
+    st = {k: v.cpu().numpy() for k, v in env.state_dict().items()}
+    slots = env.stats_buf.cpu().numpy()
+    kernel = env.kernel_name("step")
+
+    assert done.sum() > E, "episodes must finish and autoreset during the run"
+    for i, rk in enumerate(ranks):
+        off, n = int(rk["off"]), int(rk["n"])
+        assert (off, n) == gb.shard(E, i, world)
+        assert str(rk["kernel"]) == kernel
+        sl = slice(off, off + n)
+        np.testing.assert_array_equal(rk["reward"], rew[:, sl], err_msg=f"rank {i} reward")
+        np.testing.assert_array_equal(rk["done"], done[:, sl], err_msg=f"rank {i} done")
+        np.testing.assert_array_equal(rk["obs_bits"], bits[:, sl], err_msg=f"rank {i} obs")
+        for k, v in st.items():
+            want = v[:, sl] if k in ("static_obs", "dyn_obs", "dyn_goal") else v[sl]
+            np.testing.assert_array_equal(rk["state_" + k], want, err_msg=f"rank {i} state[{k}]")
+        # per-wave stats slots: a rank's slots are the one-rank run's slots of its env range
+        assert off % 64 == 0 and n % 64 == 0
+        np.testing.assert_array_equal(rk["stats_buf"], slots[off // 64:(off + n) // 64], err_msg=f"rank {i} stats")
+    # every rank gathered the same (world, 8) records: each rank's own reduction of its slots
+    for rk in ranks:
+        np.testing.assert_array_equal(rk["gathered"], ranks[0]["gathered"])
+    g = ranks[0]["gathered"]
+    for i, rk in enumerate(ranks):
+        b = torch.from_numpy(rk["stats_buf"])
+        rec = b.sum(0)
+        rec[4], rec[5] = b[:, 4].min(), b[:, 5].max()
+        np.testing.assert_array_equal(g[i], rec.numpy())
+    comb = gb.combine_stats(torch.from_numpy(g))
+    one = env.episode_stats()
+    assert comb["episodes"] == one["episodes"] and comb["min_return"] == one["min_return"]
+    assert comb["max_return"] == one["max_return"]
+    assert comb["mean_length"] == pytest.approx(one["mean_length"], rel=1e-12)
+    assert comb["mean_return"] == pytest.approx(one["mean_return"], rel=1e-12)
+    env.close()

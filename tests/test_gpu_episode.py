@@ -1,0 +1,224 @@
+"""GPU (HIP, gfx950) parity on the full default episode: the production kernels against the
+oracle through goal changes and the TimeLimit.
+
+The bench workload (EnvConfig() defaults, caller actions) runs the fixed-shape step kernel
+be_kernel<W, 0, 13, 5>, the fused be_rollout kernel and the fused be_policy_rollout kernel.
+Each has its own goal re-pick (newGoalList for pairwise-distinct goals, ballenv_env.py:339-353)
+and its own `ep_len mod (goal_change+1)` counter arithmetic, and all of them fold the gym
+TimeLimit(1000) (gym_ballenv/__init__.py:7) plus the autoreset into the step.  Random
+actions end most episodes within a few steps, so a fresh reset never reaches ep_len 50 or
+1000.  These tests therefore start every env at a random ep_len -- all goal-change phases,
+with a quarter of the envs at 990..999 so that TimeLimit truncations happen -- and compare
+every per-step output and the state with the C oracle (pinned to the reference's golden
+vectors in test_oracle_golden.py) on a 2048-env slice keyed by global env id.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from test_gpu_parity import KEYS, make_env, np_state
+
+pytestmark = pytest.mark.gpu
+
+SLICE = 2048
+
+
+def _random_lens(N, rng, limit=1000):
+    lens = rng.integers(0, limit, N).astype(np.int32)
+    near = rng.random(N) < 0.25
+    lens[near] = rng.integers(limit - 10, limit, int(near.sum()))
+    return lens
+
+
+def _slice_state(st, a, k):
+    out = {}
+    for key, v in st.items():
+        out[key] = v[:, a:a + k] if key in ("static_obs", "dyn_obs", "dyn_goal") else v[a:a + k]
+    return out
+
+
+def _setup(cfg_py, N, W, dev, a, k, seed, rng, terminal=True):
+    """GPU env (N envs) and an oracle on global envs [a, a+k), both reset and then moved to the
+    same random ep_len phase."""
+    env = make_env(cfg_py, N, W, dev, seed=seed, terminal_obs=terminal)
+    cfg = cfg_py.to_abi(k, W, env_offset=a, seed=seed)
+    st = oracle.new_state(cfg)
+    out = oracle.new_out(cfg, terminal=terminal)
+    oracle.reset(cfg, st, out)
+    env.reset()
+    lens = _random_lens(N, rng, cfg_py.time_limit or 1000)
+    env.ep_len.copy_(torch.from_numpy(lens).to(dev))
+    st["ep_len"][:] = lens[a:a + k]
+    got = _slice_state(np_state(env), a, k)
+    for key in KEYS:
+        np.testing.assert_array_equal(got[key], st[key], err_msg=f"after reset: {key}")
+    return env, cfg, st, out
+
+
+def _check_step(t, a, k, out, obs, reward, done, trunc, fret, flen, term=None):
+    sl = slice(a, a + k)
+    d = done[sl].cpu().numpy()
+    np.testing.assert_array_equal(reward[sl].cpu().numpy(), out["reward"], err_msg=f"reward t={t}")
+    np.testing.assert_array_equal(d, out["done"].astype(bool), err_msg=f"done t={t}")
+    np.testing.assert_array_equal(trunc[sl].cpu().numpy(), out["truncated"].astype(bool), err_msg=f"truncated t={t}")
+    np.testing.assert_array_equal(obs[sl].cpu().numpy(), out["obs"], err_msg=f"obs t={t}")
+    np.testing.assert_array_equal(fret[sl].cpu().numpy()[d], out["final_return"][d], err_msg=f"final_return t={t}")
+    np.testing.assert_array_equal(flen[sl].cpu().numpy()[d], out["final_len"][d], err_msg=f"final_len t={t}")
+    if term is not None:
+        np.testing.assert_array_equal(term[sl].cpu().numpy()[d], out["terminal_obs"][d], err_msg=f"terminal_obs t={t}")
+    return int(out["truncated"].sum())
+
+
+def _check_state(env, st, a, k, msg):
+    got = _slice_state(np_state(env), a, k)
+    for key in KEYS:
+        np.testing.assert_array_equal(got[key], st[key], err_msg=f"{msg}: state[{key}]")
+
+
+@pytest.mark.parametrize("W,N,a", [(10, 65536, 40960), (5, 4096, 1024), (10, 3000, 952)])
+def test_step_kernel_default_episode(gpu, W, N, a):
+    """be_step (fixed-shape kernel) at the defaults -- goal change every 51 steps, TimeLimit
+    1000, autoreset -- bit-exact against the oracle over 120 steps (>= 2 goal changes per env
+    that survives), including truncations from the TimeLimit."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig()
+    assert cfg_py.time_limit == 1000 and cfg_py.goal_change_step == 50
+    rng = np.random.default_rng(W * 7 + N)
+    k = min(SLICE, N - a)
+    env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, k, seed=0xBA11, rng=rng)
+    assert env.kernel_name("step") == f"be_kernel<{W}, 0, 13, 5>"
+    acts = env.sample_actions(120, seed=0xBA11)
+    n_trunc = n_change = 0
+    for t in range(120):
+        out["terminal_obs"][:] = 0
+        env.terminal_obs.zero_()
+        g0 = st["dyn_goal"].copy()
+        oracle.step(cfg, st, out, actions=acts[t, a:a + k].cpu().numpy())
+        n_change += int((st["dyn_goal"] != g0).any(0).sum())
+        obs, reward, done, info = env.step(acts[t])
+        n_trunc += _check_step(t, a, k, out, obs, reward, done, info["truncated"], info["final_return"],
+                               info["final_len"], info["terminal_obs"])
+        _check_state(env, st, a, k, f"t={t}")
+    assert n_trunc > 0 and n_change > 0, (n_trunc, n_change)
+    env.status()
+    env.close()
+
+
+def test_step_kernel_time_limit_boundary(gpu):
+    """Every env starts at ep_len 995..999: the TimeLimit truncates the survivors within five
+    steps and the autoreset starts their next episode (ep_len 999 -> done, ep_len 0)."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig()
+    N, W = 4096, 10
+    rng = np.random.default_rng(3)
+    env, cfg, st, out = _setup(cfg_py, N, W, gpu, 0, N, seed=99, rng=rng)
+    lens = rng.integers(995, 1000, N).astype(np.int32)
+    env.ep_len.copy_(torch.from_numpy(lens).to(gpu))
+    st["ep_len"][:] = lens
+    acts = torch.full((N,), 5, dtype=torch.uint8, device=gpu)    # (0, 0): stay put, fewer collisions
+    n_trunc = 0
+    for t in range(8):
+        out["terminal_obs"][:] = 0
+        env.terminal_obs.zero_()
+        oracle.step(cfg, st, out, actions=acts.cpu().numpy())
+        obs, reward, done, info = env.step(acts)
+        n_trunc += _check_step(t, 0, N, out, obs, reward, done, info["truncated"], info["final_return"],
+                               info["final_len"], info["terminal_obs"])
+        _check_state(env, st, 0, N, f"t={t}")
+    assert n_trunc > N // 4, n_trunc
+    assert (env.ep_len.cpu().numpy() < 10).all()
+    env.status()
+    env.close()
+
+
+@pytest.mark.parametrize("G", [0, 1, 3, 7])
+@pytest.mark.parametrize("W", [10, 5])
+def test_goal_change_steps_vs_oracle(gpu, G, W):
+    """Short goal-change periods with caller actions (so the fixed-shape kernel runs): every
+    env goes through many goal re-picks (pick + (pick >= current goal)) against the oracle."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig(goal_change_step=G)
+    N = 4096
+    rng = np.random.default_rng(100 + G)
+    env, cfg, st, out = _setup(cfg_py, N, W, gpu, 0, N, seed=G + 1, rng=rng)
+    assert env.kernel_name("step") == f"be_kernel<{W}, 0, 13, 5>"
+    acts = env.sample_actions(30, seed=G)
+    n_change = 0
+    for t in range(30):
+        out["terminal_obs"][:] = 0
+        env.terminal_obs.zero_()
+        g0 = st["dyn_goal"].copy()
+        oracle.step(cfg, st, out, actions=acts[t].cpu().numpy())
+        n_change += int((st["dyn_goal"] != g0).sum())
+        obs, reward, done, info = env.step(acts[t])
+        _check_step(t, 0, N, out, obs, reward, done, info["truncated"], info["final_return"], info["final_len"],
+                    info["terminal_obs"])
+        _check_state(env, st, 0, N, f"G={G} t={t}")
+    assert n_change > 0
+    env.status()
+    env.close()
+
+
+@pytest.mark.parametrize("W,N,a,G", [(10, 65536, 8192, 50), (5, 4096, 2048, 50), (10, 4096, 0, 3)])
+def test_rollout_kernel_default_episode(gpu, W, N, a, G):
+    """be_rollout (the fused random-action rollout) against the oracle through goal changes and
+    TimeLimit truncations: 120 steps as chunks of 50 + 70."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig(goal_change_step=G)
+    rng = np.random.default_rng(W + N + G)
+    k = min(SLICE, N - a)
+    env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, k, seed=0x5EED, rng=rng)
+    assert env.kernel_name("rollout") == f"rollout_kernel<{W}, 13, 5, 0, 1, 10>"
+    acts = env.sample_actions(120, seed=17)
+    n_trunc, t0 = 0, 0
+    for K in (50, 70):
+        obs, reward, done, info = env.rollout(acts[t0:t0 + K])
+        for j in range(K):
+            t = t0 + j
+            out["terminal_obs"][:] = 0
+            oracle.step(cfg, st, out, actions=acts[t, a:a + k].cpu().numpy())
+            n_trunc += _check_step(t, a, k, out, obs[j], reward[j], done[j], info["truncated"][j],
+                                   info["final_return"][j], info["final_len"][j], info["terminal_obs"][j])
+        t0 += K
+        _check_state(env, st, a, k, f"after step {t0}")
+    assert G != 50 or n_trunc > 0
+    env.status()
+    env.close()
+
+
+@pytest.mark.parametrize("W,N,a", [(10, 65536, 16384), (5, 4096, 0)])
+def test_policy_rollout_default_episode(gpu, W, N, a):
+    """be_policy_rollout (select_action + step fused) against the oracle stepped with the
+    actions the kernel drew: rewards, dones, recorded obs and the state after 2 x 60 steps,
+    through goal changes and TimeLimit truncations.  (The action draw itself is checked
+    against PyTorch in test_gpu_policy.py / test_gpu_rollout.py.)"""
+    from gym_ballenv_amd.config import EnvConfig
+    from gym_ballenv_amd.policy import Policy, reference_weights
+    from gym_ballenv_amd.rollout import Rollout
+    cfg_py = EnvConfig()
+    rng = np.random.default_rng(W * 13)
+    k = min(SLICE, N - a)
+    env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, k, seed=0xACE, rng=rng, terminal=False)
+    path = reference_weights(W)
+    torch.manual_seed(0)
+    pol = Policy.from_npz(path, W) if path else Policy(W)
+    T = 60
+    ro = Rollout(env, pol, horizon=T, backend="fused", record_obs=True, seed=0x5E1EC7, chunk=T)
+    n_trunc = 0
+    for h in range(2):
+        ro.run_eager()
+        acts = ro.actions[:, a:a + k].cpu().numpy()
+        np.testing.assert_array_equal(ro.obs[0, a:a + k].cpu().numpy(), out["obs"] if h else ro.obs[0, a:a + k].cpu().numpy())
+        for t in range(T):
+            oracle.step(cfg, st, out, actions=acts[t])
+            np.testing.assert_array_equal(ro.rewards[t, a:a + k].cpu().numpy(), out["reward"], err_msg=f"h={h} t={t}")
+            np.testing.assert_array_equal(ro.dones[t, a:a + k].cpu().numpy(), out["done"].astype(bool))
+            np.testing.assert_array_equal(ro.obs[t + 1, a:a + k].cpu().numpy(), out["obs"], err_msg=f"obs h={h} t={t}")
+            n_trunc += int(out["truncated"].sum())
+        _check_state(env, st, a, k, f"horizon {h}")
+        np.testing.assert_array_equal(env.obs[a:a + k].cpu().numpy(), out["obs"])
+    assert n_trunc > 0
+    env.status()
+    ro.close()
+    env.close()

@@ -15,10 +15,12 @@ step() {  # name timeout cmd...
 }
 TAG=${TAG:-run}
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -o timeout=300
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
   tail -3 gpurun_out/pytest_gpu.log
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
+step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5 ${BENCH_ARGS:-}
+tail -1 gpurun_out/bench_driver.log
 step bench 400 python bench.py ${BENCH_ARGS:-}
 tail -1 gpurun_out/bench.log
 if [ "${PROFILE:-1}" = "1" ]; then
