@@ -161,6 +161,10 @@ template <class T>
 __device__ __forceinline__ T ld_s(const T* base, uint32_t idx) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (size_t)(idx * (uint32_t)sizeof(T)));
 }
+template <class T>
+__device__ __forceinline__ T& ld_s_ptr(T* base, uint32_t idx) {   // (stores: the same addressing)
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (size_t)(idx * (uint32_t)sizeof(T)));
+}
 __device__ __forceinline__ int isqrt_small(int n) {  // floor(sqrt(n)), 0 <= n < 2^22
   int s = (int)__builtin_amdgcn_sqrtf((float)n);
   if (s * s > n) --s;
@@ -360,6 +364,10 @@ __device__ __forceinline__ void stage_row(uint8_t* stage, int tid, const uint32_
 }
 
 // Copy the block's staged rows to obs (u8) and/or obs_f32 with 16-byte stores.
+// BE_OBS_STORE (A/B diagnostics): 0 plain stores, 1 sc1 (write-through) buffer stores, 2 nt stores.
+#ifndef BE_OBS_STORE
+#define BE_OBS_STORE 0
+#endif
 template <int BLOCK>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid, int64_t row0,
                                          uint8_t* obs, float* obs_f32, int tid = (int)threadIdx.x) {
@@ -367,8 +375,22 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid
   if (obs) {
     uint8_t* dst = obs + row0 * F;
     const int nv = bytes >> 4;
+#if BE_OBS_STORE == 1
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, bytes, 0x00020000);
+    for (int v = tid; v < nv; v += BLOCK) {
+      const uint4 x = reinterpret_cast<const uint4*>(stage)[v];
+      typedef int v4i_ __attribute__((ext_vector_type(4)));
+      const v4i_ y = {(int)x.x, (int)x.y, (int)x.z, (int)x.w};
+      __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v * 16, 0, 16);   // aux 16 = sc1
+    }
+#elif BE_OBS_STORE == 2
+    typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
+    for (int v = tid; v < nv; v += BLOCK)
+      __builtin_nontemporal_store(reinterpret_cast<const v4u_*>(stage)[v], reinterpret_cast<v4u_*>(dst) + v);
+#else
     for (int v = tid; v < nv; v += BLOCK)
       reinterpret_cast<uint4*>(dst)[v] = reinterpret_cast<const uint4*>(stage)[v];
+#endif
     for (int b = (nv << 4) + tid; b < bytes; b += BLOCK) dst[b] = stage[b];
   }
   if (obs_f32) {
@@ -531,11 +553,12 @@ __device__ void reset_env_philox(const KParams& p, const Tables& t, int i, int q
 // atomics and no contention; be_stats_slots() tells the caller how many slots.
 struct WaveStats { double n, s1, s2, sl, mn, mx; };
 
-__device__ __forceinline__ WaveStats wave_stats(bool done, double ret, int len) {
+__device__ __forceinline__ WaveStats wave_stats(bool done, double ret, int len,
+                                                unsigned long long lanes = ~0ull) {
   WaveStats w{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   // wave-uniform loop over the finished lanes in lane order (deterministic; ~1 per wave per
   // step at the reference's episode lengths, so a few readlanes beat a 6-level shuffle tree)
-  for (unsigned long long m = __ballot(done); m; m &= m - 1) {
+  for (unsigned long long m = __ballot(done) & lanes; m; m &= m - 1) {
     const int l = __ffsll((long long)m) - 1;
     const unsigned long long bits = __double_as_longlong(ret);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, l);
@@ -721,7 +744,9 @@ __device__ __forceinline__ double reset_dists(int32_t ag, int32_t go, int32_t a0
 // wl: per-wave LDS scratch, >= P*(K+8) words.  Where the new state goes is the caller's:
 // osink(slot, k, il, packed xy) for obstacle k of env il (drawn by lane slot*G + k), then
 // esink(own, agent, goal, pre-resample agent) on the env's own lane, after a wave barrier.
-template <int WT, int NSC, int NDC, int PMAX, class OSink, class ESink>
+// LPE = 2 (step2_kernel): lanes 2e and 2e+1 share env e; m holds the even (owner) lanes, and
+// both lanes of a reset env take the new agent / goal / window rows (esink runs on both).
+template <int WT, int NSC, int NDC, int PMAX, class OSink, class ESink, int LPE = 1>
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
                             uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl, OSink&& osink, ESink&& esink) {
@@ -806,7 +831,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
     DIAG(13);
     int own = -1;   // the slot whose env this lane owns
 #pragma unroll
-    for (int s2 = 0; s2 < P; ++s2) own = (s2 < n && lane == ls[s2]) ? s2 : own;
+    for (int s2 = 0; s2 < P; ++s2) own = (s2 < n && lane / LPE == ls[s2] / LPE) ? s2 : own;
     if (own >= 0) {
       const int32_t ag = stash[own * 4 + 0], go = stash[own * 4 + 1], a0 = stash[own * 4 + 2];
       ax = px(ag); ay = py(ag); gx = px(go); gy = py(go);
@@ -1154,9 +1179,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
     if ((tid & 63) == 0) atomicOr(p.status, (int)f);
   }
-  WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
-  if (MODE == MODE_STEP && p.stats && !DBG(DBG_NO_STATS))
-    ws = wave_stats(done && lead, fin_ret, fin_len);  // all lanes converged here
+  WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY}, ws_hi = ws;
+  if (MODE == MODE_STEP && p.stats && !DBG(DBG_NO_STATS)) {   // all lanes converged here
+    if constexpr (FIXED) {   // one slot per 32 envs (be_stats_slots): the wave's two halves
+      ws = wave_stats(done && lead, fin_ret, fin_len, 0x00000000FFFFFFFFull);
+      ws_hi = wave_stats(done && lead, fin_ret, fin_len, 0xFFFFFFFF00000000ull);
+    } else {
+      ws = wave_stats(done && lead, fin_ret, fin_len);
+    }
+  }
 
   // ---- episode boundary
   bool do_reset = false;
@@ -1331,10 +1362,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
           }
         }
       }
-      if (p.stats && lane == 0 && ws.n > 0.0) {
-        double* slot = p.stats + ((size_t)blockIdx.x * (BLOCK_THREADS / 64) + w) * 8;
-        slot[0] += ws.n; slot[1] += ws.s1; slot[2] += ws.s2; slot[3] += ws.sl;
-        slot[4] = fmin(slot[4], ws.mn); slot[5] = fmax(slot[5], ws.mx);
+      if (p.stats && (lane == 0 || lane == 32)) {
+        const WaveStats& v = lane == 0 ? ws : ws_hi;
+        if (v.n > 0.0) {
+          double* slot = p.stats + (((size_t)blockIdx.x * (BLOCK_THREADS / 64) + w) * 2 + (lane >> 5)) * 8;
+          slot[0] += v.n; slot[1] += v.s1; slot[2] += v.s2; slot[3] += v.sl;
+          slot[4] = fmin(slot[4], v.mn); slot[5] = fmax(slot[5], v.mx);
+        }
       }
       DIAG(6);
       return;
@@ -1467,6 +1501,249 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   }
 }
 
+// ------------------------------------------------------------------ two lanes per env
+// step2_kernel<W, NS, ND>: the fixed-shape step of be_kernel<W, MODE_STEP, NS, ND>, bit for bit,
+// with TWO lanes per env: lanes 2e and 2e+1 of a wave hold env e of the wave's 32.
+//
+// At 65 536 envs one lane per env is one wave per SIMD, and a lone wave issues at most one
+// vector instruction every ~4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost')
+// while the SIMD could take one every 2: the step is bound by the length of each wave's
+// instruction chain, not by HBM.  Two lanes per env give two waves per SIMD and split the
+// per-obstacle work, so each wave's chain is shorter:
+//  * lane h of an env takes obstacles k = 2j + h (dynamic: 3 slots, static: 7; the slot past
+//    the count re-reads a real obstacle and is masked out), moves / tests / stores them and
+//    keeps its own near list;
+//  * the pair's collision flags and window rows are OR-ed with one DPP op each;
+//  * lane h writes its half of the obs row (uint2 words [7h, 7h+7)) into the wave's stage and
+//    half of the per-env scalar stores (a per-lane pointer select: one store instruction);
+//  * the Philox block, the agent move, the f64 reward and done run on both lanes (the same
+//    instruction stream, so no extra issue).
+// Autoreset is wave_resets with the even lanes as owners; stats fold per wave (32 envs =
+// one be_stats_slots slot) in env order, as be_kernel's half-wave folds do.
+__device__ __forceinline__ uint32_t pair_or(uint32_t x) {   // OR with the other lane of the pair
+  return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+}
+
+template <int WT, int NSC, int NDC>
+__global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
+  constexpr int L = 2, EPW = 64 / L, EPB = BLOCK_THREADS / L, NWAVE = BLOCK_THREADS / 64;
+  constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;   // obstacle slots per lane
+  constexpr int KR = Geo<WT>::K, F = Geo<WT>::F, NW = Geo<WT>::NW;
+  constexpr int NQ = F / 8, HQ = (NQ + 1) / 2;                     // uint2 words per row / per lane
+  static_assert(WT == 10 && F == 104 && NW == 5, "the half-row word split below is laid out for W = 10");
+  static_assert(NDC <= 5, "one Philox block of 24-bit fields");
+  static_assert(RCAP >= NWAVE * 16 && 16 * KR >= (64 / (NSC + NDC)) * (KR + 4), "wave reset scratch");
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ Tables t;
+  __shared__ uint32_t s_rows[NWAVE][16 * KR];    // wave_resets scratch (row masks + stash)
+  constexpr int TW = (int)(sizeof(Tables) / 4);
+
+  DIAG(0);
+  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & 1;
+  const int blk0 = (int)blockIdx.x * EPB, i = blk0 + (tid >> 1), e0 = blk0 + w * EPW;
+  const bool valid = i < N;
+  const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
+  NearList<BLOCK_THREADS> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
+  uint8_t* stage = smem + (size_t)(SS + SD + 1) * BLOCK_THREADS * 4 + (size_t)w * EPW * F;   // the wave's 32 rows
+
+  // ---- every load, straight-line, in use order (32-bit element offsets from uniform bases;
+  //      obstacle k of lane h at element k*N + env: pick_kernel keeps NS*N < 2^30)
+  const uint32_t tword = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid, TW - 1));
+  const uint32_t episode = ld_s(p.episode, ic);
+  const int len0 = ld_s(p.ep_len, ic);
+  const int a = ld_s(p.actions, ic);
+  const int32_t agent0 = ld_s(p.agent, ic), goal0 = ld_s(p.goal, ic);
+  int32_t dp[SD], so[SS];
+  int dgi[SD];
+#pragma unroll
+  for (int j = 0; j < SD; ++j) {
+    const uint32_t e = (uint32_t)min(L * j + h, NDC - 1) * (uint32_t)N + ic;
+    dp[j] = ld_s(p.dyn_obs, e);
+    dgi[j] = ld_s(p.dyn_goal, e);
+  }
+#pragma unroll
+  for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
+  const double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic);
+  double ret = ld_s(p.ep_return, ic);
+  reinterpret_cast<uint32_t*>(&t)[min(tid, TW - 1)] = tword;
+  __syncthreads();   // the only block barrier: tables staged (state loads retire in order as used)
+  DIAG(1);
+
+  // ---- action -> agent move + clamp (ballenv_env.py:247-259); unit moves and speeds
+  uint32_t st_flags = a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
+  const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
+  int ax = min(max(px(agent0) + (int)((p.amx >> sh) & 3u) - 1, 0), p.screen_w);
+  int ay = min(max(py(agent0) + (int)((p.amy >> sh) & 3u) - 1, 0), p.screen_h);
+  int gx = px(goal0), gy = py(goal0);
+  const Win g0(p, 0, 0);
+  const uint32_t R2 = (uint32_t)g0.R2;
+  const NearBox nb0(g0);
+  typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+  const v2s boxo = {(short)(WT / 2 + g0.R), (short)(WT / 2 + g0.R)};
+  const v2u boxw = {(unsigned short)nb0.bw, (unsigned short)nb0.bh};
+  const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
+  DIAG(8);
+
+  // ---- this lane's obstacles: move (dynamic), collision + window-box test (be_kernel's
+  //      packed int16x2 form), near list
+  int counter = (int)((double)len0 * p.inv_g1);   // counter == ep_len mod (G+1)
+  counter = len0 - counter * (p.goal_change + 1);
+  if (counter < 0) counter += p.goal_change + 1;
+  if (counter > p.goal_change) counter -= p.goal_change + 1;
+  const bool change = counter >= p.goal_change;
+  const u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+  bool hs = false, hd = false;
+  auto obstacle_pk = [&](int32_t opk, bool real, bool& hit) {
+    const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
+    hit |= real & ((uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2);
+    const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
+    const v2u over = __builtin_elementwise_sub_sat(b, boxw);   // (0, 0) iff inside the box
+    nl.base[nl.cnt * BLOCK_THREADS] = __builtin_bit_cast(uint32_t, d);
+    nl.cnt += (real & (__builtin_bit_cast(uint32_t, over) == 0u)) ? 1 : 0;
+  };
+  DIAG(7);
+  int ngs[SD];
+#pragma unroll
+  for (int j = 0; j < SD; ++j) {
+    const int k = L * j + h;
+    const bool real = k < NDC;
+    int ox = px(dp[j]), oy = py(dp[j]);
+    const uint32_t f = h ? pick_field(b0, min(L * j + 1, 4)) : pick_field(b0, L * j);
+    uint32_t fl = 0u;
+    ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[min(k, NDC - 1)], change, f, fl);
+    st_flags |= real ? fl : 0u;
+    const int32_t npk = pk(ox, oy);
+    if (valid && real) ld_s_ptr(p.dyn_obs, (uint32_t)k * (uint32_t)N + (uint32_t)i) = npk;
+    obstacle_pk(npk, real, hd);
+  }
+  if (valid && change) {   // every obstacle re-picks its goal on the same step
+#pragma unroll
+    for (int j = 0; j < SD; ++j)
+      if (L * j + h < NDC) ld_s_ptr(p.dyn_goal, (uint32_t)(L * j + h) * (uint32_t)N + (uint32_t)i) = (uint8_t)ngs[j];
+  }
+  DIAG(11);
+#pragma unroll
+  for (int j = 0; j < SS; ++j) obstacle_pk(so[j], L * j + h < NSC, hs);
+  hs = pair_or((uint32_t)hs) != 0u;
+  hd = pair_or((uint32_t)hd) != 0u;
+  DIAG(10);
+
+  // ---- distance, reward, done (ballenv_env.py:268-286, 200-229), on both lanes
+  const double dist = calc_dist(gx, gy, ax, ay);
+  double reward = 0.0 - p.time_penalty;
+  reward += (old_dist - dist) / total;
+  if (hs) reward -= p.static_penalty;          // statics come first in obstacle_list (Q3)
+  else if (hd) reward -= p.dynamic_penalty;
+  ret += reward;
+  const int len = len0 + 1;
+  const bool env_done = (dist < p.threshold_goal) || hs || hd;
+  const bool trunc = p.time_limit > 0 && len >= p.time_limit;
+  const bool done = env_done || trunc;
+  if (valid) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
+    double* pd = h ? p.ep_return : p.reward;
+    pd[i] = h ? ret : reward;
+    int32_t* pi = h ? p.ep_len : p.agent;
+    pi[i] = h ? len : pk(ax, ay);
+    uint8_t* pb = h ? p.truncated : p.done;
+    if (pb) pb[i] = (uint8_t)(h ? (trunc && !env_done) : done);
+    if (!h) p.prev_dist[i] = dist;
+    if (done) {
+      if (!h && p.final_return) p.final_return[i] = ret;
+      if (h && p.final_len) p.final_len[i] = len;
+    }
+  }
+  DIAG(2);
+  if (__ballot(st_flags != 0u)) {   // rare: OR the wave's flags, one atomic
+    uint32_t f = st_flags;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
+    if (lane == 0) atomicOr(p.status, (int)f);
+  }
+  WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
+  if (p.stats) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
+
+  // ---- episode boundary: terminal obs, then the wave-cooperative reset of the finished envs
+  uint32_t xrows[KR];
+#pragma unroll
+  for (int k = 0; k < KR; ++k) xrows[k] = 0u;
+  const bool do_reset = valid && done && p.autoreset;
+  if (do_reset && p.terminal_obs) {   // both lanes of the pair take this branch together
+    uint32_t rows[KR], flat[NW];
+    raster_rows<WT, BLOCK_THREADS, true>(nl, g0, rows, t.hw);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k]);
+    flatten<WT>(rows, flat);
+    if (!h) write_row_global<WT>(p.terminal_obs + (int64_t)i * F, flat, quadrant(ax, ay, gx, gy));
+  }
+  const unsigned long long m = __ballot(do_reset && h == 0);
+  if (m) {
+    auto osink = [&](int, int k, int il, int32_t o) {
+      if (k < NSC) {
+        (p.static_obs + (size_t)k * N)[il] = o;
+      } else {
+        (p.dyn_obs + (size_t)(k - NSC) * N)[il] = o;
+        (p.dyn_goal + (size_t)(k - NSC) * N)[il] = (uint8_t)(k - NSC);
+      }
+    };
+    auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
+      if (h) return;   // both lanes take the new agent / goal / rows; lane 0 stores the scalars
+      p.agent[i] = ag;
+      p.goal[i] = go;
+      const double td = reset_dists(ag, go, a0, p.prev_dist[i]);
+      p.total_dist[i] = td;
+      p.ep_return[i] = 0.0;
+      p.ep_len[i] = 0;
+      p.episode[i] = episode + 1u;
+    };
+    if (!(m & (m - 1)))
+      wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
+                                                                        nl.cnt, xrows, &s_rows[w][0], osink, esink);
+    else
+      wave_resets<WT, NSC, NDC, 64, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
+                                                                         nl.cnt, xrows, &s_rows[w][0], osink, esink);
+  }
+  DIAG(3);
+
+  // ---- observation (prep_state4): own near list -> rows, OR-ed over the pair, half a row each
+  {
+    uint32_t rows[KR], flat[NW];
+    raster_rows<WT, BLOCK_THREADS, true>(nl, g0, rows, t.hw);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k] | xrows[k]);
+    flatten<WT>(rows, flat);
+    const int quad = quadrant(ax, ay, gx, gy);
+    // uint2 word q of this lane is row word 2(q + 7h) .. +1: word j >= 1 expands cells
+    // 4(j-1) .. 4(j-1)+3.  c holds this lane's cells from bit 0: lane 0 cells -4.. (its word 0
+    // is the quadrant one-hot), lane 1 cells 52..
+    const unsigned long long lo = (unsigned long long)flat[0] | ((unsigned long long)flat[1] << 32);
+    const unsigned long long hi = ((unsigned long long)flat[1] >> 20) | ((unsigned long long)flat[2] << 12) |
+                                  ((unsigned long long)flat[3] << 44);
+    const unsigned long long c = h ? hi : (lo << 4);
+    auto word = [&](int jj) -> uint32_t {   // jj: this lane's word 0 .. 2*HQ-1
+      return (((uint32_t)(c >> (4 * jj)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    };
+    uint2* dst = reinterpret_cast<uint2*>(stage + (tid & 62) / 2 * F) + HQ * h;
+#pragma unroll
+    for (int q = 0; q < HQ; ++q) {
+      const uint32_t w0 = q == 0 ? (h ? word(0) : 1u << (8 * quad)) : word(2 * q);
+      if (q < NQ - HQ || !h) dst[q] = make_uint2(w0, word(2 * q + 1));
+    }
+  }
+  DIAG(4);
+  // the wave's 32 contiguous rows out (no block barrier: a wave that reset delays nobody)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  DIAG(5);
+  copy_out<64>(stage, F, max(0, min(EPW, N - e0)), (int64_t)e0, p.obs, p.obs_f32, lane);
+  if (p.stats && lane == 0 && ws.n > 0.0) {
+    double* slot = p.stats + ((size_t)blockIdx.x * NWAVE + w) * 8;
+    slot[0] += ws.n; slot[1] += ws.s1; slot[2] += ws.s2; slot[3] += ws.sl;
+    slot[4] = fmin(slot[4], ws.mn); slot[5] = fmax(slot[5], ws.mx);
+  }
+  DIAG(6);
+}
+
 // ------------------------------------------------------------------ fused multi-step rollout
 // rollout_kernel<W, NS, ND>: p.steps consecutive be_step calls of the fixed-shape kernel in one
 // launch, for a caller-given (steps, N) action tape.  Each env's state stays in registers for
@@ -1525,8 +1802,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
 #pragma unroll
   for (int j = 0; j < NSC; ++j) so[j] = ld_s(p.static_obs + (size_t)j * N, ic);
   double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic), ret = ld_s(p.ep_return, ic);
-  // stats slot of this wave (be_stats_slots: one per 64 envs; a wave past N has none)
-  double* slot = (p.stats && e0 < N) ? p.stats + ((size_t)blockIdx.x * NWAVE + w) * 8 : nullptr;
+  // stats slot of this lane's half-wave (be_stats_slots: one per 32 envs; none past N)
+  const int e32 = e0 + (lane & 32);
+  double* slot = (p.stats && e32 < N) ? p.stats + (((size_t)blockIdx.x * NWAVE + w) * 2 + (lane >> 5)) * 8 : nullptr;
   WaveStats acc{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   if (slot) acc = WaveStats{slot[0], slot[1], slot[2], slot[3], slot[4], slot[5]};
   reinterpret_cast<uint32_t*>(&t)[min(tid, TW - 1)] = tword;
@@ -1763,9 +2041,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
         if (p.final_len) p.final_len[so_n + i] = len;
       }
     }
-    if (slot) {   // the step kernel's per-wave fold, step by step (same order: bit-identical sums)
-      const WaveStats ws = wave_stats(done && valid, ret, len);
-      if (ws.n > 0.0) {
+    if (p.stats) {   // the step kernel's per-half-wave fold, step by step (same order: bit-identical sums)
+      const WaveStats lo = wave_stats(done && valid, ret, len, 0x00000000FFFFFFFFull);
+      const WaveStats hi = wave_stats(done && valid, ret, len, 0xFFFFFFFF00000000ull);
+      const WaveStats& ws = lane < 32 ? lo : hi;
+      if (slot && ws.n > 0.0) {
         acc.n += ws.n; acc.s1 += ws.s1; acc.s2 += ws.s2; acc.sl += ws.sl;
         acc.mn = fmin(acc.mn, ws.mn); acc.mx = fmax(acc.mx, ws.mx);
       }
@@ -1868,7 +2148,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     copy_out<64>(stage, F, nrows, (int64_t)e0, p.obs_last, nullptr, lane);
   }
-  if (slot && lane == 0) {
+  if (slot && (lane & 31) == 0) {
     slot[0] = acc.n; slot[1] = acc.s1; slot[2] = acc.s2; slot[3] = acc.sl; slot[4] = acc.mn; slot[5] = acc.mx;
   }
   if (__ballot(st_flags != 0u)) {
@@ -1903,13 +2183,22 @@ struct Launch { KFn fn; int epb; int lds; char name[48]; };
 // Fixed-shape step kernels for the reference's default obstacle counts (ball_cnn_ac3.py:40-41).
 constexpr int FIX_NS = 13, FIX_ND = 5;
 
-Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false) {
+Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe2_ok = false) {
   int W = c.window;
   const int F = 4 + W * W, nobs = c.num_static + c.num_dynamic;
-  Launch L{nullptr, 0, 0};
+  Launch L{nullptr, 0, 0, {0}};
   bool staged = true;
   const bool fixed = fixed_ok && mode == MODE_STEP && c.num_static == FIX_NS && c.num_dynamic == FIX_ND &&
                      c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
+  if (fixed && lpe2_ok && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
+    // two lanes per env (step2_kernel): 128 envs per block
+    L.fn = step2_kernel<10, FIX_NS, FIX_ND>;
+    L.epb = BLOCK_THREADS / 2;
+    constexpr int SLOTS = (FIX_NS + 1) / 2 + (FIX_ND + 1) / 2 + 1;
+    L.lds = SLOTS * BLOCK_THREADS * 4 + L.epb * F;
+    snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d>", FIX_NS, FIX_ND);
+    return L;
+  }
   if (fixed && W == 10) { L.fn = be_kernel<10, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
   else if (fixed && W == 5) { L.fn = be_kernel<5, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
   switch (W) {
@@ -1934,7 +2223,7 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false) {
 
 // The fused rollout kernel for the same fixed shapes (nullptr: not applicable).
 Launch pick_rollout(const be_config& c, bool fixed_ok) {
-  Launch L{nullptr, BLOCK_THREADS, 0};
+  Launch L{nullptr, BLOCK_THREADS, 0, {0}};
   const bool fixed = fixed_ok && c.num_static == FIX_NS && c.num_dynamic == FIX_ND && c.speed_x == 1 &&
                      c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
   if (fixed && c.window == 10) L.fn = rollout_kernel<10, FIX_NS, FIX_ND>;
@@ -1947,7 +2236,7 @@ Launch pick_rollout(const be_config& c, bool fixed_ok) {
 // The fused policy rollout kernel: fixed env shape and the select_action kernel's Policy(W)
 // shapes (H 208 / W 10 and H 128 / W 5, 9 actions).
 Launch pick_policy_rollout(const be_config& c, bool fixed_ok, int HT, int KS, int NO) {
-  Launch L{nullptr, BLOCK_THREADS, 0};
+  Launch L{nullptr, BLOCK_THREADS, 0, {0}};
   const bool fixed = fixed_ok && c.num_static == FIX_NS && c.num_dynamic == FIX_ND && c.speed_x == 1 &&
                      c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
   if (fixed && c.window == 10 && HT == 13 && KS == 2 && NO == 10)
@@ -1974,6 +2263,7 @@ struct be_ctx {
   bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
+  bool step_lpe1;      // BALLENV_STEP_LPE=1: the one-lane-per-env fixed step kernel instead of step2_kernel (A/B)
   char err[512];
 };
 
@@ -2106,7 +2396,7 @@ const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
   const bool fixed_ok = !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals;
   Launch L{nullptr, 0, 0, {0}};
   switch (entry) {
-    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok); break;
+    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, !ctx->step_lpe1); break;
     case BE_ENTRY_STEP_SAMPLED: L = pick_kernel(ctx->cfg, MODE_STEP, false); break;
     case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok); break;
     case BE_ENTRY_RESET: L = pick_kernel(ctx->cfg, MODE_RESET, false); break;
@@ -2120,9 +2410,9 @@ const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
 
 int64_t be_stats_slots(const be_config* c) {
   if (!c || c->num_envs < 1 || c->window < 1) return 0;
-  // one slot per wave of 64 envs: the fixed-shape step kernels settle stats per wave, the
-  // generic ones per block (fewer slots, a prefix of these)
-  return ((int64_t)c->num_envs + 63) / 64;
+  // one slot per 32 envs: the fixed-shape kernels settle stats per half-wave (LPE 1) or per
+  // wave (LPE 2), the generic ones per block (fewer slots, a prefix of these)
+  return ((int64_t)c->num_envs + 31) / 32;
 }
 
 int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
@@ -2166,6 +2456,7 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   b.inv_g1 = 1.0 / ((double)cfg->goal_change_step + 1.0);
   if (const char* d = getenv("BALLENV_DEBUG_SKIP")) b.dbg = (int32_t)strtoul(d, nullptr, 0);
   if (const char* g = getenv("BALLENV_GENERIC_KERNELS")) ctx->generic_only = atoi(g) != 0;
+  if (const char* l = getenv("BALLENV_STEP_LPE")) ctx->step_lpe1 = atoi(l) == 1;
   Tables& t = ctx->tables;
   memset(&t, 0, sizeof t);
   for (int k = 0; k < cfg->num_dynamic; ++k) t.speed[k] = cfg->obstacle_speed[k];
@@ -2248,7 +2539,7 @@ static int launch(be_ctx* ctx, int mode, KParams& a, void* stream) {
   int cur = -1;
   HIP_TRY(ctx, hipGetDevice(&cur));
   if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok);
+  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, !ctx->step_lpe1);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
   hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);

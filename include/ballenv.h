@@ -131,7 +131,7 @@ typedef struct be_out {
   uint8_t* terminal_obs;  /* (N, 4+W*W): obs of the terminal state, rows of done envs only (autoreset) */
   double* final_return;   /* (N): episode return, written for done envs only */
   int32_t* final_len;     /* (N): episode length, written for done envs only */
-  double* stats;          /* (be_stats_slots(cfg), 8) f64 accumulators, one slot per wave of 64 envs of the step
+  double* stats;          /* (be_stats_slots(cfg), 8) f64 accumulators, one slot per 32 envs of the step
                              kernel (no atomics): [0]=episodes, [1]=sum return, [2]=sum return^2,
                              [3]=sum length, [4]=min return, [5]=max return, [6..7] unused; the caller
                              initialises [4]=+inf, [5]=-inf, the rest 0, and reduces over slots */

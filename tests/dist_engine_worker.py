@@ -15,6 +15,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def start_lens(off, n):
+    """Episode phase of global envs [off, off+n): a pure function of the global env id, so every
+    split of the batch starts the same (goal changes and TimeLimit truncations inside the run)."""
+    import torch
+    g = torch.arange(off, off + n, dtype=torch.int64)
+    return ((g * 7919) % 1000).to(torch.int32)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
@@ -37,6 +45,7 @@ def main():
     off, n = gb.shard(args.envs, rank, world)
     env = gb.BatchedBallEnv(n, args.window, gb.EnvConfig(), device=dev, seed=args.seed, env_offset=off)
     env.reset()
+    env.ep_len.copy_(start_lens(off, n).to(dev))
     acts = env.sample_actions(args.steps, seed=args.seed)
     T, F = args.steps, env.obs_dim
     rew = np.empty((T, n))

@@ -2,13 +2,14 @@
 oracle through goal changes and the TimeLimit.
 
 The bench workload (EnvConfig() defaults, caller actions) runs the fixed-shape step kernel
-be_kernel<W, 0, 13, 5>, the fused be_rollout kernel and the fused be_policy_rollout kernel.
+(step2_kernel<10, 13, 5> at W=10, be_kernel<5, 0, 13, 5> at W=5), the fused be_rollout kernel
+and the fused be_policy_rollout kernel.
 Each has its own goal re-pick (newGoalList for pairwise-distinct goals, ballenv_env.py:339-353)
 and its own `ep_len mod (goal_change+1)` counter arithmetic, and all of them fold the gym
-TimeLimit(1000) (gym_ballenv/__init__.py:7) plus the autoreset into the step.  Random
-actions end most episodes within a few steps, so a fresh reset never reaches ep_len 50 or
-1000.  These tests therefore start every env at a random ep_len -- all goal-change phases,
-with a quarter of the envs at 990..999 so that TimeLimit truncations happen -- and compare
+TimeLimit(1000) (gym_ballenv/__init__.py:7) plus the autoreset into the step.  From a fresh
+reset the first goal change is 51 steps away and the TimeLimit 1000.  These tests therefore
+start every env at a random ep_len -- all goal-change phases, with a quarter of the envs at
+990..999 so that TimeLimit truncations happen within a few steps -- and compare
 every per-step output and the state with the C oracle (pinned to the reference's golden
 vectors in test_oracle_golden.py) on a 2048-env slice keyed by global env id.
 """
@@ -24,10 +25,15 @@ pytestmark = pytest.mark.gpu
 SLICE = 2048
 
 
+def fixed_step_kernel(W):
+    """The step kernel pick_kernel selects at the defaults with caller actions."""
+    return "step2_kernel<10, 13, 5>" if W == 10 else f"be_kernel<{W}, 0, 13, 5>"
+
+
 def _random_lens(N, rng, limit=1000):
     lens = rng.integers(0, limit, N).astype(np.int32)
     near = rng.random(N) < 0.25
-    lens[near] = rng.integers(limit - 10, limit, int(near.sum()))
+    lens[near] = rng.integers(max(0, limit - 10), limit, int(near.sum()))
     return lens
 
 
@@ -87,7 +93,7 @@ def test_step_kernel_default_episode(gpu, W, N, a):
     rng = np.random.default_rng(W * 7 + N)
     k = min(SLICE, N - a)
     env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, k, seed=0xBA11, rng=rng)
-    assert env.kernel_name("step") == f"be_kernel<{W}, 0, 13, 5>"
+    assert env.kernel_name("step") == fixed_step_kernel(W)
     acts = env.sample_actions(120, seed=0xBA11)
     n_trunc = n_change = 0
     for t in range(120):
@@ -142,7 +148,7 @@ def test_goal_change_steps_vs_oracle(gpu, G, W):
     N = 4096
     rng = np.random.default_rng(100 + G)
     env, cfg, st, out = _setup(cfg_py, N, W, gpu, 0, N, seed=G + 1, rng=rng)
-    assert env.kernel_name("step") == f"be_kernel<{W}, 0, 13, 5>"
+    assert env.kernel_name("step") == fixed_step_kernel(W)
     acts = env.sample_actions(30, seed=G)
     n_change = 0
     for t in range(30):
@@ -222,3 +228,47 @@ def test_policy_rollout_default_episode(gpu, W, N, a):
     env.status()
     ro.close()
     env.close()
+
+
+@pytest.mark.parametrize("N,tl", [(20000, 20), (65536, 1000), (1000, 7)])
+def test_step2_equals_one_lane_kernel(gpu, N, tl, monkeypatch):
+    """step2_kernel (two lanes per env) equals the one-lane fixed-shape kernel bit for bit --
+    obs, reward, done, truncated, final return / length, terminal obs, the state and the
+    stats slots -- through mass truncation (tl=20: every env of every wave resets on the same
+    steps) and at the defaults from random episode phases; N=20000 / 1000 leave partial blocks."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig(time_limit=tl)
+    W = 10
+    envs = []
+    for lpe in ("2", "1"):
+        monkeypatch.setenv("BALLENV_STEP_LPE", lpe)
+        envs.append(make_env(cfg_py, N, W, gpu, seed=31, terminal_obs=True))
+    monkeypatch.delenv("BALLENV_STEP_LPE")
+    assert envs[0].kernel_name("step") == "step2_kernel<10, 13, 5>"
+    assert envs[1].kernel_name("step") == "be_kernel<10, 0, 13, 5>"
+    lens = torch.from_numpy(_random_lens(N, np.random.default_rng(N), tl)).to(gpu)
+    for e in envs:
+        e.reset()
+        e.ep_len.copy_(lens)
+    acts = envs[0].sample_actions(45, seed=9)
+    n_done = 0
+    for t in range(45):
+        for e in envs:
+            e.terminal_obs.zero_()
+        res = [e.step(acts[t]) for e in envs]
+        for a, b in zip(res[0][:3], res[1][:3]):
+            np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=f"t={t}")
+        d = res[0][2].cpu().numpy()
+        n_done += int(d.sum())
+        for key in ("truncated", "terminal_obs"):
+            np.testing.assert_array_equal(res[0][3][key].cpu().numpy(), res[1][3][key].cpu().numpy(), err_msg=key)
+        for key in ("final_return", "final_len"):
+            np.testing.assert_array_equal(res[0][3][key].cpu().numpy()[d], res[1][3][key].cpu().numpy()[d])
+        s0, s1 = np_state(envs[0]), np_state(envs[1])
+        for k in KEYS:
+            np.testing.assert_array_equal(s0[k], s1[k], err_msg=f"t={t} {k}")
+    np.testing.assert_array_equal(envs[0].stats_buf.cpu().numpy(), envs[1].stats_buf.cpu().numpy())
+    assert n_done > 0
+    for e in envs:
+        e.status()
+        e.close()
