@@ -46,7 +46,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--window", type=int, default=10)
-    p.add_argument("--mode", choices=["graph", "eager"], default="graph")
+    p.add_argument("--mode", choices=["loop", "graph", "eager"], default="graph",
+                   help="loop: be_step_n, the K step launches queued by the library's C loop; graph: "
+                        "hipGraph replay of captured be_step launches; eager: one ctypes be_step call per step")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--cpu-procs", type=int, default=0, help="0 = one per usable host core")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,6 +117,15 @@ def cpu_baseline(window, seconds, procs=None):
                       f"Python); value = W={window if window in by_w else 10} aggregate"}
 
 
+def wait_spin(ev, dev):
+    """Poll the end event, then synchronize: the timed region still ends on torch.cuda.synchronize(),
+    but the host notices the GPU finishing within a poll instead of a blocking wake-up."""
+    import torch
+    while not ev.query():
+        pass
+    torch.cuda.synchronize(dev)
+
+
 def timed_graph_steps(graphs, steps, dev, stream, world):
     """Replay graphs (steps in total), bracketed by barrier + synchronize; max over ranks."""
     import torch
@@ -123,15 +134,15 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
     ev0.record(stream)
+    t0 = time.perf_counter()
     for g in graphs:
         g.replay()
     ev1.record(stream)
-    torch.cuda.synchronize(dev)
+    wait_spin(ev1, dev)
+    el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -478,23 +489,33 @@ def main():
             g.replay()
         torch.cuda.synchronize(dev)
 
+    if args.mode == "loop":   # one untimed pass of the timed command (like the graph replay above)
+        rc = lib.be_step_n(ctx, st_ref, C.c_void_p(a0), K, out_ref, s_ptr)
+        if rc:
+            _abi.check(rc, ctx)
+        torch.cuda.synchronize(dev)
+
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
     ev0.record(stream)
-    if args.mode == "graph":
+    t0 = time.perf_counter()
+    if args.mode == "loop":
+        rc = lib.be_step_n(ctx, st_ref, C.c_void_p(a0), K, out_ref, s_ptr)
+        if rc:
+            _abi.check(rc, ctx)
+    elif args.mode == "graph":
         for g in graphs:
             g.replay()            # replays on the current stream (= stream)
     else:
         for t in range(K):
             launch(t, s_ptr)
     ev1.record(stream)
-    torch.cuda.synchronize(dev)
+    wait_spin(ev1, dev)       # ... torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     n_devices = 1
     if world > 1:
         el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -542,7 +563,9 @@ def main():
                                    "13 static + 5 dynamic obstacles, TimeLimit 1000, autoreset",
                        "envs_per_gpu": N, "global_envs": N * world, "window": W,
                        "parallelism": f"env-shard x{world} (no per-step collective)",
-                       "launch": "hipGraph replay of be_step launches" if args.mode == "graph" else "eager"},
+                       "launch": {"loop": "be_step_n: K be_step launches queued by the library's C loop",
+                                  "graph": "hipGraph replay of be_step launches",
+                                  "eager": "one ctypes be_step call per step"}[args.mode]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_env_step": B, "bytes_source": "SURVEY.md 8(d): 82+8*Ns+20*Nd+4+W^2",

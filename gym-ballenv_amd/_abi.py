@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get("BALLENV_LIB") or os.path.join(os.path.dirname(os.path
 # Names declared in include/ballenv.h (checked by tests/test_abi.py).
 EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_bytes", "be_stats_slots",
            "be_last_error", "be_kernel_name",
-           "be_create", "be_destroy", "be_reset", "be_step", "be_rollout", "be_observe", "be_sample_actions",
+           "be_create", "be_destroy", "be_reset", "be_step", "be_step_n", "be_rollout", "be_observe", "be_sample_actions",
            "be_status", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
            "be_policy_rollout", "be_policy_bytes", "be_observe_blocks",
            "be_board_config_default", "be_board_create", "be_board_destroy", "be_board_last_error",
@@ -123,6 +123,7 @@ def lib() -> C.CDLL:
         "be_reset": (C.c_int, [vp, P(BeState), vp, vp, i32, P(BeOut), vp]),
         "be_step": (C.c_int, [vp, P(BeState), vp, vp, vp, P(BeOut), vp]),
         "be_rollout": (C.c_int, [vp, P(BeState), vp, C.c_int32, P(BeOut), vp]),
+        "be_step_n": (C.c_int, [vp, P(BeState), vp, C.c_int32, P(BeOut), vp]),
         "be_observe": (C.c_int, [vp, P(BeState), P(BeOut), vp]),
         "be_sample_actions": (C.c_int, [vp, vp, i32, u64, vp]),
         "be_status": (C.c_int, [vp, P(i32), vp]),

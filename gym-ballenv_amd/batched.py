@@ -218,6 +218,24 @@ class BatchedBallEnv:
             info["terminal_obs"] = term
         return obs, reward, done, info
 
+    def step_n(self, actions: torch.Tensor):
+        """``K = actions.shape[0]`` consecutive :meth:`step` calls (caller actions), queued by one
+        library call (be_step_n: one kernel launch per step from a C loop).  Returns what the
+        last :meth:`step` would: ``(obs, reward, done, info)`` of step K."""
+        a = actions if actions.dtype == torch.uint8 else actions.to(torch.uint8)
+        if a.device != self.device:
+            a = a.to(self.device)
+        a = a.contiguous()
+        if a.dim() != 2 or a.shape[1] != self.num_envs:
+            raise ValueError(f"actions must be (K, {self.num_envs}), got {tuple(a.shape)}")
+        _abi.check(self._lib.be_step_n(self._ctx, C.byref(self._st), a.data_ptr(), int(a.shape[0]),
+                                       C.byref(self._out), self._stream()), self._ctx)
+        self._keep = (a,)
+        info = {"truncated": self.truncated, "final_return": self.final_return, "final_len": self.final_len}
+        if self.terminal_obs is not None:
+            info["terminal_obs"] = self.terminal_obs
+        return (self.obs_f32 if self._want_f32 else self.obs), self.reward, self.done, info
+
     def observe(self) -> torch.Tensor:
         """prep_state4 of the current state (no state change)."""
         _abi.check(self._lib.be_observe(self._ctx, C.byref(self._st), C.byref(self._out), self._stream()), self._ctx)

@@ -161,6 +161,19 @@ template <class T>
 __device__ __forceinline__ T ld_s(const T* base, uint32_t idx) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (size_t)(idx * (uint32_t)sizeof(T)));
 }
+// Output / state stores of the fixed-shape step kernels: write-through (sc1, a relaxed agent-scope
+// atomic store), so the stores drain while the wave runs instead of in the kernel-end L2 write-back.
+#ifndef BE_WT
+#define BE_WT 1
+#endif
+template <class T>
+__device__ __forceinline__ void st_wt(T* p, T v) {
+#if BE_WT
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
 template <class T>
 __device__ __forceinline__ T& ld_s_ptr(T* base, uint32_t idx) {   // (stores: the same addressing)
   return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (size_t)(idx * (uint32_t)sizeof(T)));
@@ -364,9 +377,10 @@ __device__ __forceinline__ void stage_row(uint8_t* stage, int tid, const uint32_
 }
 
 // Copy the block's staged rows to obs (u8) and/or obs_f32 with 16-byte stores.
-// BE_OBS_STORE (A/B diagnostics): 0 plain stores, 1 sc1 (write-through) buffer stores, 2 nt stores.
+// BE_OBS_STORE: 1 (default) sc1 write-through buffer stores -- the kernel-end L2 write-back then has
+// little left to do (measured 7.8 -> 7.3 us per step at 65 536 envs); 0 plain, 2 nt (A/B builds).
 #ifndef BE_OBS_STORE
-#define BE_OBS_STORE 0
+#define BE_OBS_STORE 1
 #endif
 template <int BLOCK>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid, int64_t row0,
@@ -1075,13 +1089,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
           ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[j], change, wj[j], st_flags);
           const int32_t npk = pk(ox, oy);
           dfr_dyn[j % DN] = npk; dfr_goal[j % DN] = ngs[j];
-          if (!DEFER && valid) (p.dyn_obs + (size_t)j * N)[i] = npk;
+          if (!DEFER && valid) st_wt(p.dyn_obs + (size_t)j * N + i, npk);
           obstacle_pk(npk, hd);
         }
         dfr_change = change;   // every obstacle re-picks its goal on the same step
         if (!DEFER && valid && change) {
 #pragma unroll
-          for (int j = 0; j < NDC; ++j) (p.dyn_goal + (size_t)j * N)[i] = (uint8_t)ngs[j];
+          for (int j = 0; j < NDC; ++j) st_wt(p.dyn_goal + (size_t)j * N + i, (uint8_t)ngs[j]);
         }
         DIAG(11);
 #pragma unroll
@@ -1154,16 +1168,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       done = env_done || trunc;
       dfr_reward = reward; dfr_dist = dist; dfr_trunc = trunc && !env_done;
       if (!DEFER && lead) {
-        p.reward[i] = reward;
-        p.done[i] = (uint8_t)done;
-        if (p.truncated) p.truncated[i] = (uint8_t)(trunc && !env_done);
-        p.agent[i] = pk(ax, ay);
-        p.prev_dist[i] = dist;
-        p.ep_return[i] = ret;
-        p.ep_len[i] = len;
+        st_wt(p.reward + i, reward);
+        st_wt(p.done + i, (uint8_t)done);
+        if (p.truncated) st_wt(p.truncated + i, (uint8_t)(trunc && !env_done));
+        st_wt(p.agent + i, pk(ax, ay));
+        st_wt(p.prev_dist + i, dist);
+        st_wt(p.ep_return + i, ret);
+        st_wt(p.ep_len + i, len);
         if (done) {
-          if (p.final_return) p.final_return[i] = ret;
-          if (p.final_len) p.final_len[i] = len;
+          if (p.final_return) st_wt(p.final_return + i, ret);
+          if (p.final_len) st_wt(p.final_len + i, len);
         }
       }
       fin_ret = ret; fin_len = len;
@@ -1253,20 +1267,22 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     // a reset env's new state goes straight to HBM
     auto osink = [&](int, int k, int il, int32_t o) {
       if (k < NSC) {
-        (p.static_obs + (size_t)k * N)[il] = o;
+        st_wt(p.static_obs + (size_t)k * N + il, o);
       } else {
-        (p.dyn_obs + (size_t)(k - NSC) * N)[il] = o;
-        (p.dyn_goal + (size_t)(k - NSC) * N)[il] = (uint8_t)(k - NSC);
+        st_wt(p.dyn_obs + (size_t)(k - NSC) * N + il, o);
+        st_wt(p.dyn_goal + (size_t)(k - NSC) * N + il, (uint8_t)(k - NSC));
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
-      p.agent[i] = ag;
-      p.goal[i] = go;
-      const double td = reset_dists(ag, go, a0, p.prev_dist[i]);
-      p.total_dist[i] = td;
-      p.ep_return[i] = 0.0;
-      p.ep_len[i] = 0;
-      p.episode[i] = episode + 1u;
+      st_wt(p.agent + i, ag);
+      st_wt(p.goal + i, go);
+      double prev;
+      const double td = reset_dists(ag, go, a0, prev);
+      st_wt(p.prev_dist + i, prev);
+      st_wt(p.total_dist + i, td);
+      st_wt(p.ep_return + i, 0.0);
+      st_wt(p.ep_len + i, 0);
+      st_wt(p.episode + i, episode + 1u);
     };
     if (m && !(m & (m - 1)))
       wave_resets<WT, NSC, NDC, 1>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0],
@@ -1613,13 +1629,13 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
     ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[min(k, NDC - 1)], change, f, fl);
     st_flags |= real ? fl : 0u;
     const int32_t npk = pk(ox, oy);
-    if (valid && real) ld_s_ptr(p.dyn_obs, (uint32_t)k * (uint32_t)N + (uint32_t)i) = npk;
+    if (valid && real) st_wt(&ld_s_ptr(p.dyn_obs, (uint32_t)k * (uint32_t)N + (uint32_t)i), npk);
     obstacle_pk(npk, real, hd);
   }
   if (valid && change) {   // every obstacle re-picks its goal on the same step
 #pragma unroll
     for (int j = 0; j < SD; ++j)
-      if (L * j + h < NDC) ld_s_ptr(p.dyn_goal, (uint32_t)(L * j + h) * (uint32_t)N + (uint32_t)i) = (uint8_t)ngs[j];
+      if (L * j + h < NDC) st_wt(&ld_s_ptr(p.dyn_goal, (uint32_t)(L * j + h) * (uint32_t)N + (uint32_t)i), (uint8_t)ngs[j]);
   }
   DIAG(11);
 #pragma unroll
@@ -1641,15 +1657,15 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   const bool done = env_done || trunc;
   if (valid) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
     double* pd = h ? p.ep_return : p.reward;
-    pd[i] = h ? ret : reward;
+    st_wt(pd + i, h ? ret : reward);
     int32_t* pi = h ? p.ep_len : p.agent;
-    pi[i] = h ? len : pk(ax, ay);
+    st_wt(pi + i, h ? len : pk(ax, ay));
     uint8_t* pb = h ? p.truncated : p.done;
-    if (pb) pb[i] = (uint8_t)(h ? (trunc && !env_done) : done);
-    if (!h) p.prev_dist[i] = dist;
+    if (pb) st_wt(pb + i, (uint8_t)(h ? (trunc && !env_done) : done));
+    if (!h) st_wt(p.prev_dist + i, dist);
     if (done) {
-      if (!h && p.final_return) p.final_return[i] = ret;
-      if (h && p.final_len) p.final_len[i] = len;
+      if (!h && p.final_return) st_wt(p.final_return + i, ret);
+      if (h && p.final_len) st_wt(p.final_len + i, len);
     }
   }
   DIAG(2);
@@ -1679,21 +1695,23 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   if (m) {
     auto osink = [&](int, int k, int il, int32_t o) {
       if (k < NSC) {
-        (p.static_obs + (size_t)k * N)[il] = o;
+        st_wt(p.static_obs + (size_t)k * N + il, o);
       } else {
-        (p.dyn_obs + (size_t)(k - NSC) * N)[il] = o;
-        (p.dyn_goal + (size_t)(k - NSC) * N)[il] = (uint8_t)(k - NSC);
+        st_wt(p.dyn_obs + (size_t)(k - NSC) * N + il, o);
+        st_wt(p.dyn_goal + (size_t)(k - NSC) * N + il, (uint8_t)(k - NSC));
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
       if (h) return;   // both lanes take the new agent / goal / rows; lane 0 stores the scalars
-      p.agent[i] = ag;
-      p.goal[i] = go;
-      const double td = reset_dists(ag, go, a0, p.prev_dist[i]);
-      p.total_dist[i] = td;
-      p.ep_return[i] = 0.0;
-      p.ep_len[i] = 0;
-      p.episode[i] = episode + 1u;
+      st_wt(p.agent + i, ag);
+      st_wt(p.goal + i, go);
+      double prev;
+      const double td = reset_dists(ag, go, a0, prev);
+      st_wt(p.prev_dist + i, prev);
+      st_wt(p.total_dist + i, td);
+      st_wt(p.ep_return + i, 0.0);
+      st_wt(p.ep_len + i, 0);
+      st_wt(p.episode + i, episode + 1u);
     };
     if (!(m & (m - 1)))
       wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
@@ -2531,7 +2549,8 @@ static KParams make_params(be_ctx* ctx, const be_state* st, const be_out* out) {
   return a;
 }
 
-static int launch(be_ctx* ctx, int mode, KParams& a, void* stream) {
+// steps > 1 (be_step_n): `steps` launches of the same kernel, actions advancing by N per step.
+static int launch(be_ctx* ctx, int mode, KParams& a, void* stream, int32_t steps = 1) {
   const bool fixed_ok = mode == MODE_STEP && a.tape == nullptr && a.actions != nullptr && !ctx->generic_only &&
                         ctx->unit_moves && ctx->distinct_goals;
   if (((uintptr_t)a.obs & 15) || ((uintptr_t)a.obs_f32 & 15))
@@ -2542,7 +2561,10 @@ static int launch(be_ctx* ctx, int mode, KParams& a, void* stream) {
   const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, !ctx->step_lpe1);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
-  hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
+  for (int32_t s = 0; s < steps; ++s) {
+    hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
+    a.actions += N;
+  }
   HIP_TRY(ctx, hipGetLastError());
   return BE_OK;
 }
@@ -2569,6 +2591,18 @@ int be_step(be_ctx* ctx, const be_state* st, const uint8_t* actions, const int16
   KParams a = make_params(ctx, st, out);
   a.actions = actions; a.deltas = action_deltas; a.tape = draw_tape;
   return launch(ctx, MODE_STEP, a, stream);
+}
+
+int be_step_n(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t steps, const be_out* out,
+              void* stream) {
+  if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
+  if (int rc = check_state(ctx, st)) return rc;
+  if (!actions || steps < 0) return fail(ctx, BE_E_INVALID, "%s", "be_step_n needs actions and steps >= 0");
+  if (!out || !out->reward || !out->done) return fail(ctx, BE_E_INVALID, "%s", "be_step_n needs out->reward and out->done");
+  if (steps == 0) return BE_OK;
+  KParams a = make_params(ctx, st, out);
+  a.actions = actions;
+  return launch(ctx, MODE_STEP, a, stream, steps);
 }
 
 int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t steps, const be_out* out,

@@ -196,6 +196,14 @@ int be_step(be_ctx* ctx, const be_state* st, const uint8_t* actions, const int16
 int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t steps, const be_out* out,
                void* stream);
 
+/* `steps` be_step launches (one kernel per step, caller actions + s*N) queued from a host loop
+ * in the library, with the same `out` every step: out holds the last step's outputs (and
+ * stats accumulate) exactly as after `steps` be_step calls.  The reference's counterpart is
+ * the caller's per-step loop (examples/ball_cnn_ac3.py:573-600): this is that loop for every
+ * env, minus the per-call Python overhead.                                             */
+int be_step_n(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t steps, const be_out* out,
+              void* stream);
+
 /* prep_state4 of the current state of every env (no state change). */
 int be_observe(be_ctx* ctx, const be_state* st, const be_out* out, void* stream);
 

@@ -272,3 +272,28 @@ def test_step2_equals_one_lane_kernel(gpu, N, tl, monkeypatch):
     for e in envs:
         e.status()
         e.close()
+
+
+def test_step_n_equals_step_calls(gpu):
+    """be_step_n (K launches queued by one call) leaves the same state, last-step outputs and
+    stats slots as K be_step calls."""
+    from gym_ballenv_amd.config import EnvConfig
+    N, W, K = 6000, 10, 37
+    envs = [make_env(EnvConfig(), N, W, gpu, seed=5) for _ in range(2)]
+    lens = torch.from_numpy(_random_lens(N, np.random.default_rng(1))).to(gpu)
+    for e in envs:
+        e.reset()
+        e.ep_len.copy_(lens)
+    acts = envs[0].sample_actions(K, seed=2)
+    for t in range(K):
+        ra = envs[0].step(acts[t])
+    rb = envs[1].step_n(acts)
+    for x, y in zip(ra[:3], rb[:3]):
+        np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+    sa, sb = np_state(envs[0]), np_state(envs[1])
+    for k in KEYS:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    np.testing.assert_array_equal(envs[0].stats_buf.cpu().numpy(), envs[1].stats_buf.cpu().numpy())
+    for e in envs:
+        e.status()
+        e.close()
