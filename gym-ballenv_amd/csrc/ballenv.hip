@@ -764,12 +764,14 @@ template <int WT, int NSC, int NDC, int PMAX, class OSink, class ESink, int LPE 
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
                             uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl, OSink&& osink, ESink&& esink) {
-  constexpr int K = Geo<WT>::K, G = NSC + NDC, P = (64 / G < PMAX) ? 64 / G : PMAX;
+  // G + 1 lanes per env: lane k < G draws obstacle k, lane G the goal / agent block; every lane
+  // runs ONE Philox chain, and the goal lane's four values reach the slot's lanes by readlane
+  constexpr int K = Geo<WT>::K, G = NSC + NDC, GL = G + 1, P = (64 / GL < PMAX) ? 64 / GL : PMAX;
   static_assert(P >= 1, "one env's obstacles must fit a wave");
   const int lane = (int)(threadIdx.x & 63);
   const int W = p.screen_w, H = p.screen_h;
   const int rx = t.radius_obstacle + t.radius_agent, ry2 = t.radius_obstacle + 2 * t.radius_agent;
-  const int slot = lane / G, k = lane - slot * G;
+  const int slot = lane / GL, k = lane - slot * GL;
   uint32_t* wrows = wl;            // [P][K] row masks
   int* stash = reinterpret_cast<int*>(wl + P * K);   // [P][4]: agent xy, goal xy, pre-resample agent xy packed
   while (m) {
@@ -796,22 +798,36 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
     // compiler must keep them in program order (a memory fence would also drain the stores)
     asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    if (act) {
-      // goal / agent (ballenv_env.py:115-126) and obstacle k's first attempt (:131-164),
-      // drawn together: neither depends on the other's result
-      const u4 b0 = philox(u, ep, 0u, tag(PURPOSE_RESET, 0), p.seed);
-      const bool is_static = k < NSC;
-      const uint32_t sub0 = is_static ? ((1u << 22) | ((uint32_t)k << 12)) : ((2u << 22) | ((uint32_t)(k - NSC) << 12));
-      u4 bo = philox(u, ep, 0u, tag(PURPOSE_RESET, sub0), p.seed);
-      const int rgx = map_range(b0.x, W - t.strip_goal_x, W), rgy = map_range(b0.y, H - t.strip_goal_y, H);
-      int rax = map_range(b0.z, 0, t.strip_agent_x), ray = map_range(b0.w, 0, t.strip_agent_y);
-      const int ax0 = rax, ay0 = ray;
+    // one Philox block per lane: obstacle k's first attempt (ballenv_env.py:131-164), or the
+    // goal / agent block (:115-126) on the slot's lane G
+    const bool is_goal = k == G, is_static = k < NSC;
+    const uint32_t sub0 = is_goal ? 0u
+                        : is_static ? ((1u << 22) | ((uint32_t)k << 12)) : ((2u << 22) | ((uint32_t)(k - NSC) << 12));
+    u4 bo = philox(u, ep, 0u, tag(PURPOSE_RESET, sub0), p.seed);
+    int rgx = 0, rgy = 0, rax = 0, ray = 0, ax0 = 0, ay0 = 0;
+    if (act && is_goal) {
+      rgx = map_range(bo.x, W - t.strip_goal_x, W); rgy = map_range(bo.y, H - t.strip_goal_y, H);
+      rax = map_range(bo.z, 0, t.strip_agent_x); ray = map_range(bo.w, 0, t.strip_agent_y);
+      ax0 = rax; ay0 = ray;
       for (int r = 0; d2i(rgx - rax, rgy - ray) < p.min_spawn_d2; ++r) {   // dist < 50 <=> d2 < 2500 (integers)
         if (r >= REJECT_LIMIT - 1) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
         const u4 b = philox(u, ep, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
         rax = map_range(b.x, 0, t.strip_agent_x); ray = map_range(b.y, 0, t.strip_agent_y);
       }
-      DIAG(12);
+    }
+    {   // the slot's goal / agent to all its lanes (uniform readlanes, one select per slot)
+      const int32_t gp = pk(rgx, rgy), apk = pk(rax, ray);
+      int32_t gsel = 0, asel = 0;
+#pragma unroll
+      for (int s2 = 0; s2 < P; ++s2) {
+        const int32_t g2 = __builtin_amdgcn_readlane(gp, s2 * GL + G), a2 = __builtin_amdgcn_readlane(apk, s2 * GL + G);
+        gsel = slot == s2 ? g2 : gsel; asel = slot == s2 ? a2 : asel;
+      }
+      if (is_goal && act) stash[slot * 4 + 2] = pk(ax0, ay0);
+      rgx = px(gsel); rgy = py(gsel); rax = px(asel); ray = py(asel);
+    }
+    DIAG(12);
+    if (act && !is_goal) {
       int ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
       int oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
       if (is_static) {        // rejection vs the agent / goal rectangles (:145, :193-197)
@@ -826,18 +842,19 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
         }
       }
       osink(slot, k, il, pk(ox, oy));
-      if (k == 0) {
-        stash[slot * 4 + 0] = pk(rax, ray); stash[slot * 4 + 1] = pk(rgx, rgy); stash[slot * 4 + 2] = pk(ax0, ay0);
-      }
+      if (k == 0) { stash[slot * 4 + 0] = pk(rax, ray); stash[slot * 4 + 1] = pk(rgx, rgy); }
       const int f = ox - (rax - WT / 2), e = oy - (ray - WT / 2);   // unit cell step (fixed-shape kernels)
       if ((uint32_t)(f + rx) <= (uint32_t)(WT - 1 + 2 * rx) && (uint32_t)(e + rx) <= (uint32_t)(K - 1 + 2 * rx)) {
+        uint32_t mk[K];   // few lanes get here: the row masks branch-free, then same-address LDS atomics
 #pragma unroll
-        for (int r = 0; r < K; ++r) {   // few lanes get here: same-address LDS atomics stay cheap
+        for (int r = 0; r < K; ++r) {
           const int ady = abs(e - r);
           const int hw = t.hw[min(ady, HW_MAX)];
           const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
-          if (ady <= rx && lo <= hi) atomicOr(&wrows[slot * K + r], (2u << hi) - (1u << lo));
+          mk[r] = (ady <= rx && lo <= hi) ? (2u << hi) - (1u << lo) : 0u;
         }
+#pragma unroll
+        for (int r = 0; r < K; ++r) atomicOr(&wrows[slot * K + r], mk[r]);
       }
     }
     asm volatile("" ::: "memory");
@@ -1542,13 +1559,14 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t x) {   // OR with the other
 
 template <int WT, int NSC, int NDC>
 __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
-  constexpr int L = 2, EPW = 64 / L, EPB = BLOCK_THREADS / L, NWAVE = BLOCK_THREADS / 64;
+  constexpr int CT = BLOCK_THREADS;
+  constexpr int L = 2, EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
   constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;   // obstacle slots per lane
   constexpr int KR = Geo<WT>::K, F = Geo<WT>::F, NW = Geo<WT>::NW;
   constexpr int NQ = F / 8, HQ = (NQ + 1) / 2;                     // uint2 words per row / per lane
   static_assert(WT == 10 && F == 104 && NW == 5, "the half-row word split below is laid out for W = 10");
   static_assert(NDC <= 5, "one Philox block of 24-bit fields");
-  static_assert(RCAP >= NWAVE * 16 && 16 * KR >= (64 / (NSC + NDC)) * (KR + 4), "wave reset scratch");
+  static_assert(16 * KR >= (64 / (NSC + NDC)) * (KR + 4), "wave reset scratch");
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ Tables t;
   __shared__ uint32_t s_rows[NWAVE][16 * KR];    // wave_resets scratch (row masks + stash)
@@ -1557,10 +1575,11 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   DIAG(0);
   const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & 1;
   const int blk0 = (int)blockIdx.x * EPB, i = blk0 + (tid >> 1), e0 = blk0 + w * EPW;
+  uint8_t* stage_blk = smem + (size_t)(SS + SD + 1) * CT * 4;   // [EPB envs][F]
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
-  NearList<BLOCK_THREADS> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
-  uint8_t* stage = smem + (size_t)(SS + SD + 1) * BLOCK_THREADS * 4 + (size_t)w * EPW * F;   // the wave's 32 rows
+  NearList<CT> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
+  uint8_t* stage = stage_blk + (size_t)w * EPW * F;   // the wave's 32 rows
 
   // ---- every load, straight-line, in use order (32-bit element offsets from uniform bases;
   //      obstacle k of lane h at element k*N + env: pick_kernel keeps NS*N < 2^30)
@@ -1581,6 +1600,15 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
   const double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic);
   double ret = ld_s(p.ep_return, ic);
+  // the wave's stats slot (one per 32 envs), read now: a wave with a finished env updates it at
+  // the very end, and a dependent load there would lengthen exactly the waves that reset
+  double* const slot = p.stats ? p.stats + ((size_t)blockIdx.x * NWAVE + w) * 8 : nullptr;
+  double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sp2 = sp0;
+  if (slot && lane == 0 && e0 < N) {
+    sp0 = reinterpret_cast<const double2*>(slot)[0];
+    sp1 = reinterpret_cast<const double2*>(slot)[1];
+    sp2 = reinterpret_cast<const double2*>(slot)[2];
+  }
   reinterpret_cast<uint32_t*>(&t)[min(tid, TW - 1)] = tword;
   __syncthreads();   // the only block barrier: tables staged (state loads retire in order as used)
   DIAG(1);
@@ -1614,11 +1642,12 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
     hit |= real & ((uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2);
     const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
     const v2u over = __builtin_elementwise_sub_sat(b, boxw);   // (0, 0) iff inside the box
-    nl.base[nl.cnt * BLOCK_THREADS] = __builtin_bit_cast(uint32_t, d);
+    nl.base[nl.cnt * CT] = __builtin_bit_cast(uint32_t, d);
     nl.cnt += (real & (__builtin_bit_cast(uint32_t, over) == 0u)) ? 1 : 0;
   };
   DIAG(7);
   int ngs[SD];
+  int32_t dnew[SD];
 #pragma unroll
   for (int j = 0; j < SD; ++j) {
     const int k = L * j + h;
@@ -1628,14 +1657,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
     uint32_t fl = 0u;
     ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[min(k, NDC - 1)], change, f, fl);
     st_flags |= real ? fl : 0u;
-    const int32_t npk = pk(ox, oy);
-    if (valid && real) st_wt(&ld_s_ptr(p.dyn_obs, (uint32_t)k * (uint32_t)N + (uint32_t)i), npk);
-    obstacle_pk(npk, real, hd);
-  }
-  if (valid && change) {   // every obstacle re-picks its goal on the same step
-#pragma unroll
-    for (int j = 0; j < SD; ++j)
-      if (L * j + h < NDC) st_wt(&ld_s_ptr(p.dyn_goal, (uint32_t)(L * j + h) * (uint32_t)N + (uint32_t)i), (uint8_t)ngs[j]);
+    dnew[j] = pk(ox, oy);
+    obstacle_pk(dnew[j], real, hd);
   }
   DIAG(11);
 #pragma unroll
@@ -1655,6 +1678,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   const bool env_done = (dist < p.threshold_goal) || hs || hd;
   const bool trunc = p.time_limit > 0 && len >= p.time_limit;
   const bool done = env_done || trunc;
+  const bool do_reset = valid && done && p.autoreset;
   if (valid) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
     double* pd = h ? p.ep_return : p.reward;
     st_wt(pd + i, h ? ret : reward);
@@ -1667,6 +1691,15 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
       if (!h && p.final_return) st_wt(p.final_return + i, ret);
       if (h && p.final_len) st_wt(p.final_len + i, len);
     }
+    // (stored after done is known: measured faster than storing inside the obstacle loop)
+#pragma unroll
+    for (int j = 0; j < SD; ++j) {
+      const int k = L * j + h;
+      if (k < NDC) {
+        st_wt(&ld_s_ptr(p.dyn_obs, (uint32_t)k * (uint32_t)N + (uint32_t)i), dnew[j]);
+        if (change) st_wt(&ld_s_ptr(p.dyn_goal, (uint32_t)k * (uint32_t)N + (uint32_t)i), (uint8_t)ngs[j]);
+      }
+    }
   }
   DIAG(2);
   if (__ballot(st_flags != 0u)) {   // rare: OR the wave's flags, one atomic
@@ -1675,24 +1708,23 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
     for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
     if (lane == 0) atomicOr(p.status, (int)f);
   }
+  const unsigned long long m = __ballot(do_reset && h == 0);
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
-  if (p.stats) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
+  if (slot) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
 
-  // ---- episode boundary: terminal obs, then the wave-cooperative reset of the finished envs
+  // ---- episode boundary: terminal obs, then the reset of the finished envs
   uint32_t xrows[KR];
 #pragma unroll
   for (int k = 0; k < KR; ++k) xrows[k] = 0u;
-  const bool do_reset = valid && done && p.autoreset;
   if (do_reset && p.terminal_obs) {   // both lanes of the pair take this branch together
     uint32_t rows[KR], flat[NW];
-    raster_rows<WT, BLOCK_THREADS, true>(nl, g0, rows, t.hw);
+    raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
 #pragma unroll
     for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k]);
     flatten<WT>(rows, flat);
     if (!h) write_row_global<WT>(p.terminal_obs + (int64_t)i * F, flat, quadrant(ax, ay, gx, gy));
   }
-  const unsigned long long m = __ballot(do_reset && h == 0);
-  if (m) {
+  if (m) {   // wave-cooperative: this wave runs its own resets
     auto osink = [&](int, int k, int il, int32_t o) {
       if (k < NSC) {
         st_wt(p.static_obs + (size_t)k * N + il, o);
@@ -1725,7 +1757,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   // ---- observation (prep_state4): own near list -> rows, OR-ed over the pair, half a row each
   {
     uint32_t rows[KR], flat[NW];
-    raster_rows<WT, BLOCK_THREADS, true>(nl, g0, rows, t.hw);
+    raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
 #pragma unroll
     for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k] | xrows[k]);
     flatten<WT>(rows, flat);
@@ -1754,10 +1786,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   DIAG(5);
   copy_out<64>(stage, F, max(0, min(EPW, N - e0)), (int64_t)e0, p.obs, p.obs_f32, lane);
-  if (p.stats && lane == 0 && ws.n > 0.0) {
-    double* slot = p.stats + ((size_t)blockIdx.x * NWAVE + w) * 8;
-    slot[0] += ws.n; slot[1] += ws.s1; slot[2] += ws.s2; slot[3] += ws.sl;
-    slot[4] = fmin(slot[4], ws.mn); slot[5] = fmax(slot[5], ws.mx);
+  if (slot && lane == 0 && ws.n > 0.0) {
+    reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
+    reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
+    reinterpret_cast<double2*>(slot)[2] = make_double2(fmin(sp2.x, ws.mn), fmax(sp2.y, ws.mx));
   }
   DIAG(6);
 }
@@ -2209,7 +2241,7 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe
   const bool fixed = fixed_ok && mode == MODE_STEP && c.num_static == FIX_NS && c.num_dynamic == FIX_ND &&
                      c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
   if (fixed && lpe2_ok && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
-    // two lanes per env (step2_kernel): 128 envs per block
+    // two lanes per env (step2_kernel): 32 envs per wave, 128 per block
     L.fn = step2_kernel<10, FIX_NS, FIX_ND>;
     L.epb = BLOCK_THREADS / 2;
     constexpr int SLOTS = (FIX_NS + 1) / 2 + (FIX_ND + 1) / 2 + 1;
