@@ -166,6 +166,9 @@ __device__ __forceinline__ T ld_s(const T* base, uint32_t idx) {
 #ifndef BE_WT
 #define BE_WT 1
 #endif
+#ifndef BE_RO_STORE
+#define BE_RO_STORE 0   // the fused rollouts' per-step obs rows: plain stores (A/B builds: 1 = sc1)
+#endif
 template <class T>
 __device__ __forceinline__ void st_wt(T* p, T v) {
 #if BE_WT
@@ -382,14 +385,14 @@ __device__ __forceinline__ void stage_row(uint8_t* stage, int tid, const uint32_
 #ifndef BE_OBS_STORE
 #define BE_OBS_STORE 1
 #endif
-template <int BLOCK>
+template <int BLOCK, int SF = BE_OBS_STORE>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid, int64_t row0,
                                          uint8_t* obs, float* obs_f32, int tid = (int)threadIdx.x) {
   const int bytes = nvalid * F;
   if (obs) {
     uint8_t* dst = obs + row0 * F;
     const int nv = bytes >> 4;
-#if BE_OBS_STORE == 1
+    if constexpr (SF == 1) {
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, bytes, 0x00020000);
     for (int v = tid; v < nv; v += BLOCK) {
       const uint4 x = reinterpret_cast<const uint4*>(stage)[v];
@@ -397,14 +400,14 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid
       const v4i_ y = {(int)x.x, (int)x.y, (int)x.z, (int)x.w};
       __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v * 16, 0, 16);   // aux 16 = sc1
     }
-#elif BE_OBS_STORE == 2
+    } else if constexpr (SF == 2) {
     typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
     for (int v = tid; v < nv; v += BLOCK)
       __builtin_nontemporal_store(reinterpret_cast<const v4u_*>(stage)[v], reinterpret_cast<v4u_*>(dst) + v);
-#else
+    } else {
     for (int v = tid; v < nv; v += BLOCK)
       reinterpret_cast<uint4*>(dst)[v] = reinterpret_cast<const uint4*>(stage)[v];
-#endif
+    }
     for (int b = (nv << 4) + tid; b < bytes; b += BLOCK) dst[b] = stage[b];
   }
   if (obs_f32) {
@@ -583,6 +586,26 @@ __device__ __forceinline__ WaveStats wave_stats(bool done, double ret, int len,
     w.mn = fmin(w.mn, r); w.mx = fmax(w.mx, r);
   }
   return w;
+}
+
+// Both half-waves' folds (slots of 32 envs) from ONE ballot loop: lanes 0..31 into lo, 32..63
+// into hi, each in lane order from zero -- the same sums as two masked wave_stats calls.
+__device__ __forceinline__ void wave_stats2(bool done, double ret, int len, WaveStats& lo, WaveStats& hi) {
+  lo = WaveStats{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
+  hi = lo;
+  for (unsigned long long m = __ballot(done); m; m &= m - 1) {
+    const int l = __ffsll((long long)m) - 1;
+    const unsigned long long bits = __double_as_longlong(ret);
+    const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, l);
+    const uint32_t rh = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), l);
+    const double r = __longlong_as_double((long long)(((unsigned long long)rh << 32) | rl));
+    const double dn = (double)__builtin_amdgcn_readlane(len, l);
+    if (l < 32) {   // (uniform branch; no runtime-selected reference, which would go to scratch)
+      lo.n += 1.0; lo.s1 += r; lo.s2 += r * r; lo.sl += dn; lo.mn = fmin(lo.mn, r); lo.mx = fmax(lo.mx, r);
+    } else {
+      hi.n += 1.0; hi.s1 += r; hi.s2 += r * r; hi.sl += dn; hi.mn = fmin(hi.mn, r); hi.mx = fmax(hi.mx, r);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ lane groups
@@ -1213,8 +1236,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY}, ws_hi = ws;
   if (MODE == MODE_STEP && p.stats && !DBG(DBG_NO_STATS)) {   // all lanes converged here
     if constexpr (FIXED) {   // one slot per 32 envs (be_stats_slots): the wave's two halves
-      ws = wave_stats(done && lead, fin_ret, fin_len, 0x00000000FFFFFFFFull);
-      ws_hi = wave_stats(done && lead, fin_ret, fin_len, 0xFFFFFFFF00000000ull);
+      wave_stats2(done && lead, fin_ret, fin_len, ws, ws_hi);
     } else {
       ws = wave_stats(done && lead, fin_ret, fin_len);
     }
@@ -1626,6 +1648,10 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   const v2s boxo = {(short)(WT / 2 + g0.R), (short)(WT / 2 + g0.R)};
   const v2u boxw = {(unsigned short)nb0.bw, (unsigned short)nb0.bh};
   const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
+  // the distance and the distance term of the reward (ballenv_env.py:268-275) right after the
+  // move: the f64 sqrt / divide chain then overlaps the Philox draw and the obstacle work
+  const double dist = calc_dist(gx, gy, ax, ay);
+  const double rbase = (0.0 - p.time_penalty) + (old_dist - dist) / total;
   DIAG(8);
 
   // ---- this lane's obstacles: move (dynamic), collision + window-box test (be_kernel's
@@ -1668,9 +1694,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   DIAG(10);
 
   // ---- distance, reward, done (ballenv_env.py:268-286, 200-229), on both lanes
-  const double dist = calc_dist(gx, gy, ax, ay);
-  double reward = 0.0 - p.time_penalty;
-  reward += (old_dist - dist) / total;
+  double reward = rbase;
   if (hs) reward -= p.static_penalty;          // statics come first in obstacle_list (Q3)
   else if (hd) reward -= p.dynamic_penalty;
   ret += reward;
@@ -2071,6 +2095,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     for (int j = 0; j < NSC; ++j) obstacle_pk(so[j], hs);
 
     // ---- distance, reward, done (ballenv_env.py:268-286, 200-229)
+    // (computing this right after the move, as step2_kernel does, measured slower here)
     const double dist = calc_dist(gx, gy, ax, ay);
     double reward = 0.0 - p.time_penalty;
     reward += (old_dist - dist) / total;
@@ -2092,12 +2117,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       }
     }
     if (p.stats) {   // the step kernel's per-half-wave fold, step by step (same order: bit-identical sums)
-      const WaveStats lo = wave_stats(done && valid, ret, len, 0x00000000FFFFFFFFull);
-      const WaveStats hi = wave_stats(done && valid, ret, len, 0xFFFFFFFF00000000ull);
-      const WaveStats& ws = lane < 32 ? lo : hi;
-      if (slot && ws.n > 0.0) {
-        acc.n += ws.n; acc.s1 += ws.s1; acc.s2 += ws.s2; acc.sl += ws.sl;
-        acc.mn = fmin(acc.mn, ws.mn); acc.mx = fmax(acc.mx, ws.mx);
+      WaveStats lo, hi;
+      wave_stats2(done && valid, ret, len, lo, hi);
+      const bool lh = lane < 32;   // this lane's half (per-field selects: no runtime-selected struct)
+      const double wn = lh ? lo.n : hi.n;
+      if (slot && wn > 0.0) {
+        acc.n += wn; acc.s1 += lh ? lo.s1 : hi.s1; acc.s2 += lh ? lo.s2 : hi.s2; acc.sl += lh ? lo.sl : hi.sl;
+        acc.mn = fmin(acc.mn, lh ? lo.mn : hi.mn); acc.mx = fmax(acc.mx, lh ? lo.mx : hi.mx);
       }
     }
 
@@ -2164,7 +2190,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      copy_out<64>(stage, F, nrows, (int64_t)e0, p.obs + so_n * F, nullptr, lane);
+      copy_out<64, BE_RO_STORE>(stage, F, nrows, (int64_t)e0, p.obs + so_n * F, nullptr, lane);
       // the next step's stage writes must follow this step's stage reads (LDS ops issue in order)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -2196,7 +2222,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    copy_out<64>(stage, F, nrows, (int64_t)e0, p.obs_last, nullptr, lane);
+    copy_out<64, BE_RO_STORE>(stage, F, nrows, (int64_t)e0, p.obs_last, nullptr, lane);
   }
   if (slot && (lane & 31) == 0) {
     slot[0] = acc.n; slot[1] = acc.s1; slot[2] = acc.s2; slot[3] = acc.sl; slot[4] = acc.mn; slot[5] = acc.mx;
