@@ -19,7 +19,7 @@ steps = int(argv[argv.index("--steps") + 1])
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     f = glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True)[0]
-    rows = [r for r in csv.DictReader(open(f)) if re.search(rf"be_kernel<{window}, 0[,>]", r["Kernel_Name"])
+    rows = [r for r in csv.DictReader(open(f)) if re.search(rf"(be_kernel<{window}, 0[,>]|step2_kernel<{window}, )", r["Kernel_Name"])
             and r["Counter_Name"] == c]
     kname = rows[0]["Kernel_Name"] if rows else None
     per = {}
