@@ -117,7 +117,8 @@ enum : uint32_t { DBG_NO_STATS = 1, DBG_NO_RASTER = 2, DBG_NO_OBS = 4, DBG_NO_PH
                   DBG_NO_NEAR = 32, DBG_EXIT_ENTRY = 64, DBG_EXIT_BARRIER = 128, DBG_EXIT_PHYSICS = 256,
                   DBG_EXIT_RASTER = 512, DBG_WAIT_LOADS = 1024,
                   // fused policy rollout: every env on the table / no select_action tail / no block barriers
-                  DBG_POL_TABLE = 2048, DBG_POL_NO_FINISH = 4096, DBG_POL_NO_SYNC = 8192 };
+                  DBG_POL_TABLE = 2048, DBG_POL_NO_FINISH = 4096, DBG_POL_NO_SYNC = 8192,
+                  DBG_NO_RESET = 16384, DBG_NO_COPY = 32768 };
 #if defined(BE_DIAG_STAMPS) || defined(BE_DIAG_SKIP)
 #define DBG(x) (p.dbg & (x))
 #else
@@ -165,6 +166,16 @@ __device__ __forceinline__ T ld_s(const T* base, uint32_t idx) {
 // atomic store), so the stores drain while the wave runs instead of in the kernel-end L2 write-back.
 #ifndef BE_WT
 #define BE_WT 1
+#endif
+#ifndef BE_S2_CT
+#define BE_S2_CT 256        // step2_kernel: threads per block (A/B)
+#endif
+constexpr int S2_CT = BE_S2_CT;
+#ifndef BE_S2_LOADORDER
+#define BE_S2_LOADORDER 0   // step2_kernel: prev_dist / total_dist loaded before the obstacles (A/B)
+#endif
+#ifndef BE_S2_SCHED
+#define BE_S2_SCHED 0       // step2_kernel: scheduling barrier right after the block barrier (A/B)
 #endif
 #ifndef BE_RO_STORE
 #define BE_RO_STORE 0   // the fused rollouts' per-step obs rows: plain stores (A/B builds: 1 = sc1)
@@ -388,6 +399,11 @@ __device__ __forceinline__ void stage_row(uint8_t* stage, int tid, const uint32_
 template <int BLOCK, int SF = BE_OBS_STORE>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid, int64_t row0,
                                          uint8_t* obs, float* obs_f32, int tid = (int)threadIdx.x) {
+  if constexpr (BLOCK == 64) {   // a wave's own rows: row0 / nvalid are wave-uniform -- say so, or the
+    nvalid = __builtin_amdgcn_readfirstlane(nvalid);   // buffer descriptor lands in VGPRs and every
+    row0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)row0 >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)row0));   // store runs a waterfall loop
+  }
   const int bytes = nvalid * F;
   if (obs) {
     uint8_t* dst = obs + row0 * F;
@@ -420,6 +436,22 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid
     }
     for (int b = (nv << 2) + tid; b < bytes; b += BLOCK) dst[b] = (float)stage[b];
   }
+}
+
+// A wave's NV16 staged 16-byte words to dst (wave-uniform) in one unrolled pass: every LDS read
+// is issued before the first store, so the copy pays one LDS latency instead of one per word.
+template <int NV16, int SF = BE_OBS_STORE>
+__device__ __forceinline__ void copy_wave_full(const uint8_t* stage, uint8_t* dst, int lane) {
+  constexpr int IT = (NV16 + 63) / 64;
+  typedef int v4i_ __attribute__((ext_vector_type(4)));
+  v4i_ x[IT];
+#pragma unroll
+  for (int j = 0; j < IT; ++j) x[j] = reinterpret_cast<const v4i_*>(stage)[min(lane + 64 * j, NV16 - 1)];
+  // branch-free tail: the descriptor's size is NV16 * 16 bytes, so the buffer unit drops the
+  // stores of lanes past the end (no divergent second copy of the store sequence)
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, NV16 * 16, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < IT; ++j) __builtin_amdgcn_raw_buffer_store_b128(x[j], rsrc, (lane + 64 * j) * 16, 0, SF == 1 ? 16 : 0);
 }
 
 // Generic-W (runtime W, no staging) obs writer: per cell over the near list.
@@ -1580,8 +1612,8 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t x) {   // OR with the other
 }
 
 template <int WT, int NSC, int NDC>
-__global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
-  constexpr int CT = BLOCK_THREADS;
+__global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
+  constexpr int CT = S2_CT;
   constexpr int L = 2, EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
   constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;   // obstacle slots per lane
   constexpr int KR = Geo<WT>::K, F = Geo<WT>::F, NW = Geo<WT>::NW;
@@ -1595,6 +1627,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   constexpr int TW = (int)(sizeof(Tables) / 4);
 
   DIAG(0);
+  if (DBG(DBG_EXIT_ENTRY)) return;
   const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & 1;
   const int blk0 = (int)blockIdx.x * EPB, i = blk0 + (tid >> 1), e0 = blk0 + w * EPW;
   uint8_t* stage_blk = smem + (size_t)(SS + SD + 1) * CT * 4;   // [EPB envs][F]
@@ -1605,11 +1638,18 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
 
   // ---- every load, straight-line, in use order (32-bit element offsets from uniform bases;
   //      obstacle k of lane h at element k*N + env: pick_kernel keeps NS*N < 2^30)
-  const uint32_t tword = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid, TW - 1));
+  constexpr int TL = (TW + CT - 1) / CT;   // table words per thread (1 at 256 threads)
+  uint32_t tword[TL];
+#pragma unroll
+  for (int j = 0; j < TL; ++j)
+    tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid + j * CT, TW - 1));
   const uint32_t episode = ld_s(p.episode, ic);
   const int len0 = ld_s(p.ep_len, ic);
   const int a = ld_s(p.actions, ic);
   const int32_t agent0 = ld_s(p.agent, ic), goal0 = ld_s(p.goal, ic);
+#if BE_S2_LOADORDER
+  const double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic);
+#endif
   int32_t dp[SD], so[SS];
   int dgi[SD];
 #pragma unroll
@@ -1620,7 +1660,9 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   }
 #pragma unroll
   for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
+#if !BE_S2_LOADORDER
   const double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic);
+#endif
   double ret = ld_s(p.ep_return, ic);
   // the wave's stats slot (one per 32 envs), read now: a wave with a finished env updates it at
   // the very end, and a dependent load there would lengthen exactly the waves that reset
@@ -1631,9 +1673,14 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
     sp1 = reinterpret_cast<const double2*>(slot)[1];
     sp2 = reinterpret_cast<const double2*>(slot)[2];
   }
-  reinterpret_cast<uint32_t*>(&t)[min(tid, TW - 1)] = tword;
+#pragma unroll
+  for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tid + j * CT, TW - 1)] = tword[j];
   __syncthreads();   // the only block barrier: tables staged (state loads retire in order as used)
+#if BE_S2_SCHED
+  __builtin_amdgcn_sched_barrier(0);   // keep the barrier here: nothing that waits on later loads ahead of it
+#endif
   DIAG(1);
+  if (DBG(DBG_EXIT_BARRIER)) return;
 
   // ---- action -> agent move + clamp (ballenv_env.py:247-259); unit moves and speeds
   uint32_t st_flags = a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
@@ -1732,7 +1779,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
     for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
     if (lane == 0) atomicOr(p.status, (int)f);
   }
-  const unsigned long long m = __ballot(do_reset && h == 0);
+  if (DBG(DBG_EXIT_PHYSICS)) return;
+  const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && h == 0);
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   if (slot) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
 
@@ -1777,6 +1825,8 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
                                                                          nl.cnt, xrows, &s_rows[w][0], osink, esink);
   }
   DIAG(3);
+  if (DBG(DBG_NO_OBS)) return;
+  if (DBG(DBG_NO_RASTER)) nl.cnt = 0;
 
   // ---- observation (prep_state4): own near list -> rows, OR-ed over the pair, half a row each
   {
@@ -1809,7 +1859,13 @@ __global__ __launch_bounds__(BLOCK_THREADS, 2) void step2_kernel(KParams p) {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   DIAG(5);
-  copy_out<64>(stage, F, max(0, min(EPW, N - e0)), (int64_t)e0, p.obs, p.obs_f32, lane);
+  if (!DBG(DBG_NO_COPY)) {
+    const int e0u = __builtin_amdgcn_readfirstlane(e0);
+    if (e0u + EPW <= N && p.obs && !p.obs_f32)   // the common case: a full wave, u8 obs only
+      copy_wave_full<EPW * F / 16>(stage, p.obs + (size_t)e0u * F, lane);
+    else
+      copy_out<64>(stage, F, max(0, min(EPW, N - e0u)), (int64_t)e0u, p.obs, p.obs_f32, lane);
+  }
   if (slot && lane == 0 && ws.n > 0.0) {
     reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
     reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
@@ -2254,7 +2310,7 @@ KFn kernel_for(int mode) {
                            : (mode == MODE_RESET ? be_kernel<WT, MODE_RESET> : be_kernel<WT, MODE_OBSERVE>);
 }
 
-struct Launch { KFn fn; int epb; int lds; char name[48]; };
+struct Launch { KFn fn; int epb; int lds; char name[48]; int threads = BLOCK_THREADS; };
 
 // Fixed-shape step kernels for the reference's default obstacle counts (ball_cnn_ac3.py:40-41).
 constexpr int FIX_NS = 13, FIX_ND = 5;
@@ -2269,9 +2325,10 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe
   if (fixed && lpe2_ok && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
     // two lanes per env (step2_kernel): 32 envs per wave, 128 per block
     L.fn = step2_kernel<10, FIX_NS, FIX_ND>;
-    L.epb = BLOCK_THREADS / 2;
+    L.epb = S2_CT / 2;
+    L.threads = S2_CT;
     constexpr int SLOTS = (FIX_NS + 1) / 2 + (FIX_ND + 1) / 2 + 1;
-    L.lds = SLOTS * BLOCK_THREADS * 4 + L.epb * F;
+    L.lds = SLOTS * S2_CT * 4 + L.epb * F;
     snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d>", FIX_NS, FIX_ND);
     return L;
   }
@@ -2618,7 +2675,7 @@ static int launch(be_ctx* ctx, int mode, KParams& a, void* stream, int32_t steps
   if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
   const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, !ctx->step_lpe1);
   const int N = ctx->cfg.num_envs;
-  const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
+  const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)L.threads);
   for (int32_t s = 0; s < steps; ++s) {
     hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
     a.actions += N;

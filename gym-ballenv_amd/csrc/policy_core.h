@@ -255,7 +255,11 @@ __device__ __forceinline__ int policy_pick(const float* cdf, const float* lp, in
   act = act > last_nz ? last_nz : act;
   float la = lp[0];
 #pragma unroll
-  for (int o = 1; o < NO - 1; ++o) la = o == act ? lp[o] : la;
+  for (int o = 1; o < NO - 1; ++o) {
+    la = o == act ? lp[o] : la;
+    // a select chain the compiler would otherwise turn into lp[act] on a scratch copy of lp
+    asm volatile("" : "+v"(la));
+  }
   log_prob = la;
   return act;
 }

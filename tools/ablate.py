@@ -40,6 +40,29 @@ def time_env(env, acts, launches=100):
     return d[len(d) // 2]
 
 
+def time_graph(env, acts, launches=200):
+    """Per-launch time of `launches` back-to-back be_step launches replayed from one HIP graph
+    (the bench's launch mode), events around the replay."""
+    lib = _abi.lib()
+    st, out = C.byref(env._st), C.byref(env._out)
+    if not hasattr(env, "_abl_graph"):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=torch.cuda.Stream()):
+            sp = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+            for t in range(launches):
+                lib.be_step(env._ctx, st, C.c_void_p(acts.data_ptr() + (t % 64) * env.num_envs), None, None, out, sp)
+        env._abl_graph = g
+        g.replay()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(s)
+    env._abl_graph.replay()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / launches
+
+
 def main():
     masks = [int(m, 0) for m in os.environ.get("MASKS", "0,1,2,6,8,16,24,32,63").split(",")]
     sizes = [int(n) for n in os.environ.get("SIZES", "65536,262144,1048576").split(",")]
@@ -48,7 +71,7 @@ def main():
     res = {k: [] for k in envs}
     for _ in range(5):
         for k, (e, a) in envs.items():
-            res[k].append(time_env(e, a))
+            res[k].append(time_graph(e, a) if os.environ.get("GRAPH") else time_env(e, a))
     for (n, m), v in sorted(res.items()):
         v.sort()
         print(json.dumps({"envs": n, "mask": m, "us_median": round(v[len(v) // 2], 2), "us_min": round(v[0], 2),
