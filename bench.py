@@ -120,15 +120,6 @@ def cpu_baseline(window, seconds, procs=None):
                       f"Python); value = W={window if window in by_w else 10} aggregate"}
 
 
-def wait_spin(ev, dev):
-    """Poll the end event, then synchronize: the timed region still ends on torch.cuda.synchronize(),
-    but the host notices the GPU finishing within a poll instead of a blocking wake-up."""
-    import torch
-    while not ev.query():
-        pass
-    torch.cuda.synchronize(dev)
-
-
 def timed_graph_steps(graphs, steps, dev, stream, world):
     """Replay graphs (steps in total), bracketed by barrier + synchronize; max over ranks."""
     import torch
@@ -142,7 +133,7 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
     for g in graphs:
         g.replay()
     ev1.record(stream)
-    wait_spin(ev1, dev)
+    torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
@@ -533,7 +524,7 @@ def main():
         for t in range(K):
             launch(t, s_ptr)
     ev1.record(stream)
-    wait_spin(ev1, dev)       # ... torch.cuda.synchronize()
+    torch.cuda.synchronize(dev)   # (measured: a spin on the end event first adds ~1.5 us, tools/sync_cost.py)
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()

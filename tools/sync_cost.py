@@ -91,6 +91,69 @@ def region(kind, end):
     return el, ev0.elapsed_time(ev1) * 1e3
 
 
+hip = C.CDLL("libamdhip64.so")
+hip.hipGraphLaunch.argtypes = [C.c_void_p, C.c_void_p]
+gexec = C.c_void_p(g.raw_cuda_graph_exec())
+
+
+def host_call(kind):
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if kind == "graph":
+        g.replay()
+    else:
+        assert hip.hipGraphLaunch(gexec, sp) == 0
+    t1 = time.perf_counter()
+    torch.cuda.synchronize(dev)
+    return t1 - t0
+
+
+print("host time of g.replay()          %.2f us" % med(lambda: host_call("graph"), 50))
+print("host time of hipGraphLaunch()    %.2f us" % med(lambda: host_call("raw"), 50))
+
+
+def region_raw():
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    ev0.record(stream)
+    t0 = time.perf_counter()
+    assert hip.hipGraphLaunch(gexec, sp) == 0
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1) * 1e3
+
+
+r = [region_raw() for _ in range(30)]
+print("raw   end=sync   wall %.1f us  events %.1f us" % (statistics.median(x for x, _ in r) * 1e6,
+                                                         statistics.median(y for _, y in r)))
+def capture(t0, t1):
+    gg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gg, stream=cap):
+        cs = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        for t in range(t0, t1):
+            lib.be_step(ctx, st, C.c_void_p(acts[t].data_ptr()), None, None, out, cs)
+    gg.replay()
+    torch.cuda.synchronize(dev)
+    return gg
+
+
+for head in (1, 2, 4):
+    parts = [capture(0, head), capture(head, K)]
+
+    def region_split():
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        ev0.record(stream)
+        t0 = time.perf_counter()
+        for gg in parts:
+            gg.replay()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0, ev0.elapsed_time(ev1) * 1e3
+
+    r = [region_split() for _ in range(30)]
+    print("split %d+%d  wall %.1f us  events %.1f us" % (head, K - head, statistics.median(x for x, _ in r) * 1e6,
+                                                       statistics.median(y for _, y in r)))
 for kind in ("graph", "loop"):
     for end in ("spin", "stream", "sync"):
         r = [region(kind, end) for _ in range(30)]
