@@ -277,14 +277,26 @@ def policy_roofline(args, gb, dev, rank, pol, us_per_step, chunk, img):
     # state read+write (161 B at the defaults) and the packed policy image (per workgroup) once per launch
     B_state = gb.step_bytes(gb.EnvConfig(), W) - (1 + 8 + 1 + 4 + W * W)
     B = 18 + B_state / chunk + (img * nb) / (chunk * N)
-    return {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TOP/s", "frac": achieved / peak,
-            "traffic": None, "tiles_per_step": tiles_per_step, "lit_env_frac": lit_frac,
-            "mfma_per_tile": mfma_per_tile, "int8_ops_issued_per_step": ops_step,
-            "hbm_bytes_per_env_step": B, "hbm_GBs": B * N / (us_per_step * 1e-6) / 1e9,
-            "hbm_frac": B * N / (us_per_step * 1e-6) / 1e9 / HBM_PEAK_GBS,
-            "limiter": "neither roofline: issue/latency-bound at 4 waves per SIMD (the env physics, the per-step "
-                       "block barrier + list + draw, then the dense tiles of the few lit envs); PMC counters in "
-                       "profiles/r02_pmc_policy_rollout.json"}
+    res = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TOP/s", "frac": achieved / peak,
+           "traffic": None, "tiles_per_step": tiles_per_step, "lit_env_frac": lit_frac,
+           "mfma_per_tile": mfma_per_tile, "int8_ops_issued_per_step": ops_step,
+           "hbm_bytes_per_env_step": B, "hbm_GBs": B * N / (us_per_step * 1e-6) / 1e9,
+           "hbm_frac": B * N / (us_per_step * 1e-6) / 1e9 / HBM_PEAK_GBS,
+           "limiter": "neither roofline: VALU-issue/latency-bound at one wave per SIMD (the 89-KB policy image in "
+                      "LDS leaves room for one 4-wave block per CU): env physics, select_action's softmax/draw and "
+                      "the head FMAs of the dense tiles"}
+    # counters of the same kernel / envs / chunk (tools/pmc_passes.sh + tools/pmc_report.py, committed profile)
+    pmc = os.path.join(ROOT, "profiles", "r02_pmc_policy_rollout.json")
+    if os.path.exists(pmc):
+        d = json.load(open(pmc))
+        if d.get("units_per_dispatch") == N * chunk and f"rollout_kernel<{W}, 13, 5, {HT}, {KS}," in (d.get("kernel") or ""):
+            res.update({"traffic": d["hbm_bytes_per_unit"] * N, "traffic_per_env_step": d["hbm_bytes_per_unit"],
+                        "valu_active_frac": d.get("valu_active_per_simd_frac_est"),
+                        "mfma_busy_frac": d.get("mfma_busy_frac_est"),
+                        "lds_bank_conflict_frac": d.get("lds_bank_conflict_frac"),
+                        "wave_cycle_split": d.get("wave_cycle_split"),
+                        "pmc_source": "committed profile " + os.path.relpath(pmc, ROOT)})
+    return res
 
 
 def rollout_leg(args, gb, dev, rank, world, stream):

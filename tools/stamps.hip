@@ -75,9 +75,11 @@ int main(int argc, char** argv) {
     std::vector<std::vector<double>> sub(4);
     for (int w = 0; w < DW; ++w) {
       if (!rt[w * DP + 0] || !cy[w * DP + 8]) continue;
+      // step2_kernel stamps 8 -> 7 (Philox) -> 11 (dynamic) -> 10 (static), no point 9
+      const unsigned long long c9 = cy[w * DP + 9] ? cy[w * DP + 9] : cy[w * DP + 11];
       sub[0].push_back((double)(cy[w * DP + 8] - cy[w * DP + 1]));
-      sub[1].push_back((double)(cy[w * DP + 9] - cy[w * DP + 8]));
-      sub[2].push_back((double)(cy[w * DP + 10] - cy[w * DP + 9]));
+      sub[1].push_back((double)(c9 - cy[w * DP + 8]));
+      sub[2].push_back((double)(cy[w * DP + 10] - c9));
       sub[3].push_back((double)(cy[w * DP + 2] - cy[w * DP + 10]));
     }
     const char* sn[4] = {"  physics: action+move", "  physics: dynamic obs", "  physics: static obs", "  physics: reward+stores"};
@@ -89,7 +91,7 @@ int main(int argc, char** argv) {
       if (!rt[w * DP + 0] || !cy[w * DP + 7] || !cy[w * DP + 11]) continue;
       fx[0].push_back((double)(cy[w * DP + 7] - cy[w * DP + 8]));
       fx[1].push_back((double)(cy[w * DP + 11] - cy[w * DP + 7]));
-      fx[2].push_back((double)(cy[w * DP + 9] - cy[w * DP + 11]));
+      fx[2].push_back((double)((cy[w * DP + 9] ? cy[w * DP + 9] : cy[w * DP + 10]) - cy[w * DP + 11]));
     }
     // waves that ran resets in THIS launch: coop (generic): 4 -> 12 phase A, 12 -> 13 B, 13 -> 14 C;
     // wave resets (fixed-shape): 2 -> 12 draws, 12 -> 13 obstacles + raster, 13 -> 14 owner stores
