@@ -374,7 +374,7 @@ def test_compat_single_env(gpu):
     assert ob.shape == (1, 29) and ob.dtype == torch.float32 and float(ob[0, :4].sum()) == 1.0
     assert env.unwrapped.radius_rand_person == 20 and env.action_space.n == 9
     img = env.render(mode="rgb_array")
-    assert img.shape == (501, 501, 3)
+    assert img.shape == (500, 500, 3) and img.dtype == np.uint8   # the reference's 500x500 viewer
     for _ in range(1100):
         _, _, d, _ = env.step((0, 0))
         if d:
