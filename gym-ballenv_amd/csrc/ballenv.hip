@@ -142,8 +142,20 @@ __device__ __forceinline__ void diag_stamp(int point) {
   }
 }
 #define DIAG(pt) diag_stamp(pt)
+// per-phase cycle accumulators of a multi-step kernel: PH_INIT once, PH(k) at the end of phase k
+// (adds the cycles since the previous PH), PH_STORE at the end -> g_diag_cy[wave][k]
+#define PH_INIT unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ph_t = __builtin_amdgcn_s_memtime()
+#define PH(k) do { const unsigned long long ph_n = __builtin_amdgcn_s_memtime(); ph_acc[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
+#define PH_STORE do { \
+    const int ph_w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64); \
+    if ((threadIdx.x & 63) == 0 && ph_w < DIAG_WAVES) \
+      for (int ph_k = 0; ph_k < 8; ++ph_k) g_diag_cy[ph_w][ph_k] = ph_acc[ph_k]; \
+  } while (0)
 #else
 #define DIAG(pt) ((void)0)
+#define PH_INIT ((void)0)
+#define PH(k) ((void)0)
+#define PH_STORE ((void)0)
 #endif
 
 // ------------------------------------------------------------------ helpers
@@ -1970,6 +1982,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   const v2s boxo = {(short)bxo, (short)byo};
   const v2u boxw = {(unsigned short)nb0.bw, (unsigned short)nb0.bh};
 
+  PH_INIT;
   for (int s = 0; s < p.steps; ++s) {
     const size_t so_n = (size_t)s * N;
     // next step's action (tape mode): in flight while this step runs
@@ -1990,7 +2003,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
         my_k = atomicAdd(&cnt3[c3], 1);
         list[my_k] = (int16_t)tid;
       }
+      PH(0);
       if (!DBG(DBG_POL_NO_SYNC)) __syncthreads();   // list complete (and every wave's stage rows written)
+      PH(1);
       const int cnt = cnt3[c3];
       if (tid == 0) cnt3[c3 == 0 ? 2 : c3 - 1] = 0;   // (s + 2) % 3
       const int g4 = lane >> 4;
@@ -2059,7 +2074,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
             }
           }
         }
+        PH(2);
         __syncthreads();   // every chunk of the round's tiles
+        PH(3);
         if (ntiles <= NWAVE) break;   // one round (the common case): each env reads its chunks below
         if (tid < nt * 16 && r0 * 16 + tid < cnt) {   // one thread per listed env: the chunks in order
           const int e = list[r0 * 16 + tid];
@@ -2108,6 +2125,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       }
     }
     const int gx = px(goal), gy = py(goal);
+    PH(4);
     // ---- action -> agent move + clamp (ballenv_env.py:247-259)
     st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
     const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
@@ -2178,6 +2196,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       }
     }
 
+    PH(5);
     // ---- autoreset: new state stashed in LDS, picked up into this lane's registers
     uint32_t xrows[KR];
 #pragma unroll
@@ -2209,6 +2228,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
         wave_resets<WT, NSC, NDC, 64>(p, t, m, i, gid, episode, ax, ay, gxr, gyr, nl.cnt, xrows, &s_rows[w][0], osink, esink);
     }
 
+    PH(6);
     // ---- observation (prep_state4) into this wave's stage, then 64 rows out
     {
       const Win g(p, ax, ay);
@@ -2248,8 +2268,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     a = a_next;
+    PH(7);
   }
 
+  PH_STORE;
   // ---- state back to HBM, once
   if (valid) {
     p.agent[i] = pk(ax, ay);
