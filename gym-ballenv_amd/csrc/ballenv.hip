@@ -2261,7 +2261,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      copy_out<64, BE_RO_STORE>(stage, F, nrows, (int64_t)e0, p.obs + so_n * F, nullptr, lane);
+      if (nrows == 64)   // a full wave (wave-uniform): one unrolled pass, reads ahead of stores
+        copy_wave_full<64 * F / 16, BE_RO_STORE>(stage, p.obs + (so_n + (size_t)__builtin_amdgcn_readfirstlane(e0)) * F, lane);
+      else
+        copy_out<64, BE_RO_STORE>(stage, F, nrows, (int64_t)e0, p.obs + so_n * F, nullptr, lane);
       // the next step's stage writes must follow this step's stage reads (LDS ops issue in order)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -2295,7 +2298,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    copy_out<64, BE_RO_STORE>(stage, F, nrows, (int64_t)e0, p.obs_last, nullptr, lane);
+    if (nrows == 64)
+      copy_wave_full<64 * F / 16, BE_RO_STORE>(stage, p.obs_last + (size_t)__builtin_amdgcn_readfirstlane(e0) * F, lane);
+    else
+      copy_out<64, BE_RO_STORE>(stage, F, nrows, (int64_t)e0, p.obs_last, nullptr, lane);
   }
   if (slot && (lane & 31) == 0) {
     slot[0] = acc.n; slot[1] = acc.s1; slot[2] = acc.s2; slot[3] = acc.sl; slot[4] = acc.mn; slot[5] = acc.mx;
