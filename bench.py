@@ -352,12 +352,19 @@ def rollout_leg(args, gb, dev, rank, world, stream):
            "kernel_us_per_step": us_step, "bytes_per_env_step": B,
            "achieved_GBs": B * N / (us_step * 1e-6) / 1e9,
            "frac": B * N / (us_step * 1e-6) / 1e9 / HBM_PEAK_GBS}
-    # HBM-side bytes per env-step of the same kernel / envs / chunk (tools/pmc_kernel.py passes)
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_rollout_kernel.json")
-    if os.path.exists(pmc):
+    # HBM-side bytes per env-step of the same kernel / envs / chunk (committed PMC passes, used only
+    # when they were taken on the kernel this run launched)
+    kname = env.kernel_name("rollout")
+    res["kernel"] = kname
+    for f in ("r02_pmc_rollout_kernel.json", "r01_pmc_rollout_kernel.json"):
+        pmc = os.path.join(ROOT, "profiles", f)
+        if not os.path.exists(pmc):
+            continue
         d = json.load(open(pmc))
-        if d.get("units_per_dispatch") == N * Kc and f"rollout_kernel<{W}, 13, 5, 0," in (d.get("kernel") or ""):
-            res.update({"traffic_per_env_step": d["hbm_bytes_per_unit"], "traffic_source": os.path.relpath(pmc, ROOT)})
+        if d.get("units_per_dispatch") == N * Kc and f"::{kname}(" in (d.get("kernel") or ""):
+            res.update({"traffic_per_env_step": d["hbm_bytes_per_unit"],
+                        "traffic_source": "committed profile " + os.path.relpath(pmc, ROOT)})
+            break
     env.close()
     return res
 
