@@ -1788,8 +1788,6 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   }
   if (DBG(DBG_EXIT_PHYSICS)) return;
   const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && h == 0);
-  WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
-  if (slot) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
 
   // ---- episode boundary: terminal obs, then the reset of the finished envs
   uint32_t xrows[KR];
@@ -1873,6 +1871,10 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     else
       copy_out<64>(stage, F, max(0, min(EPW, N - e0u)), (int64_t)e0u, p.obs, p.obs_f32, lane);
   }
+  // the episode statistics fold after the obs stores are issued: off the path to the last store
+  // (6.55 -> 6.45 us; a reset leaves this lane's ret / len registers as the finished episode's)
+  WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
+  if (slot && !DBG(DBG_NO_STATS)) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
   if (slot && lane == 0 && ws.n > 0.0) {
     reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
     reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
