@@ -2421,7 +2421,7 @@ struct be_ctx {
   bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
-  bool step_lpe1;      // BALLENV_STEP_LPE=1: the one-lane-per-env fixed step kernel instead of step2_kernel (A/B)
+  bool step_lpe1;      // the one-lane-per-env fixed step kernel instead of step2_kernel (see below)
   char err[512];
 };
 
@@ -2614,6 +2614,16 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   b.inv_g1 = 1.0 / ((double)cfg->goal_change_step + 1.0);
   if (const char* d = getenv("BALLENV_DEBUG_SKIP")) b.dbg = (int32_t)strtoul(d, nullptr, 0);
   if (const char* g = getenv("BALLENV_GENERIC_KERNELS")) ctx->generic_only = atoi(g) != 0;
+  {  // Two lanes per env (step2_kernel) shorten each wave's dependent chain where one lane per env
+     // leaves at most ~1.5 waves per SIMD; past that the one-lane kernel has the waves to hide its
+     // latency and the pair's duplicated per-env work costs more than it saves (measured on MI355X,
+     // 256 CUs: step2 6.42 / 7.51 us at 65 536 / 98 304 envs against 6.97 / 7.92; one lane 8.13 /
+     // 14.5 / 48.9 us at 131 072 / 262 144 / 2^20 against 8.54 / 16.2 / 52.6).
+     // BALLENV_STEP_LPE=1 / 2 forces one or two lanes (A/B).
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    ctx->step_lpe1 = (int64_t)cfg->num_envs > (int64_t)96 * 4 * cus;
+  }
   if (const char* l = getenv("BALLENV_STEP_LPE")) ctx->step_lpe1 = atoi(l) == 1;
   Tables& t = ctx->tables;
   memset(&t, 0, sizeof t);

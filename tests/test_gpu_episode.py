@@ -230,6 +230,23 @@ def test_policy_rollout_default_episode(gpu, W, N, a):
     env.close()
 
 
+def test_step_kernel_dispatch_by_batch(gpu, monkeypatch):
+    """W=10 steps on step2_kernel up to 1.5 waves per SIMD of one-lane work (96 x 4 x CUs envs,
+    98 304 on a 256-CU MI355X) and on the one-lane kernel past it; BALLENV_STEP_LPE overrides."""
+    from gym_ballenv_amd.config import EnvConfig
+    monkeypatch.delenv("BALLENV_STEP_LPE", raising=False)
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    cut = 96 * 4 * cus
+    for N, name in ((cut, "step2_kernel<10, 13, 5>"), (cut + 64, "be_kernel<10, 0, 13, 5>")):
+        e = make_env(EnvConfig(), N, 10, gpu, seed=1)
+        assert e.kernel_name("step") == name, (N, cus)
+        e.close()
+    monkeypatch.setenv("BALLENV_STEP_LPE", "2")
+    e = make_env(EnvConfig(), cut + 64, 10, gpu, seed=1)
+    assert e.kernel_name("step") == "step2_kernel<10, 13, 5>"
+    e.close()
+
+
 @pytest.mark.parametrize("N,tl", [(20000, 20), (65536, 1000), (1000, 7)])
 def test_step2_equals_one_lane_kernel(gpu, N, tl, monkeypatch):
     """step2_kernel (two lanes per env) equals the one-lane fixed-shape kernel bit for bit --
