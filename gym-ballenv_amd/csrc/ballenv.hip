@@ -402,6 +402,9 @@ __device__ __forceinline__ void stage_row(uint8_t* stage, int tid, const uint32_
 #ifndef BE_OBS_STORE
 #define BE_OBS_STORE 1
 #endif
+#ifndef BE_OBS_AUX
+#define BE_OBS_AUX 16   // copy_wave_full's cache-policy bits at BE_OBS_STORE 1 (gfx950: sc0 1, nt 2, sc1 16)
+#endif
 template <int BLOCK, int SF = BE_OBS_STORE>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid, int64_t row0,
                                          uint8_t* obs, float* obs_f32, int tid = (int)threadIdx.x) {
@@ -457,7 +460,7 @@ __device__ __forceinline__ void copy_wave_full(const uint8_t* stage, uint8_t* ds
   // stores of lanes past the end (no divergent second copy of the store sequence)
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, NV16 * 16, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < IT; ++j) __builtin_amdgcn_raw_buffer_store_b128(x[j], rsrc, (lane + 64 * j) * 16, 0, SF == 1 ? 16 : 0);
+  for (int j = 0; j < IT; ++j) __builtin_amdgcn_raw_buffer_store_b128(x[j], rsrc, (lane + 64 * j) * 16, 0, SF == 1 ? BE_OBS_AUX : 0);
 }
 
 // Generic-W (runtime W, no staging) obs writer: per cell over the near list.
@@ -2338,7 +2341,11 @@ KFn kernel_for(int mode) {
 struct Launch { KFn fn; int epb; int lds; char name[48]; int threads = BLOCK_THREADS; };
 
 // Fixed-shape step kernels for the reference's default obstacle counts (ball_cnn_ac3.py:40-41).
-constexpr int FIX_NS = 13, FIX_ND = 5;
+#ifndef BE_FIX_NS            // the reference's obstacle counts; other values only in diagnostics builds
+#define BE_FIX_NS 13
+#define BE_FIX_ND 5
+#endif
+constexpr int FIX_NS = BE_FIX_NS, FIX_ND = BE_FIX_ND;
 
 Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe2_ok = false) {
   int W = c.window;

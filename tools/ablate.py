@@ -18,7 +18,8 @@ from gym_ballenv_amd import _abi  # noqa: E402
 
 def make(n, w, dbg):
     os.environ["BALLENV_DEBUG_SKIP"] = str(dbg)
-    env = gb.BatchedBallEnv(n, w, gb.EnvConfig(), device="cuda:0", seed=1)
+    ns, nd = (int(x) for x in os.environ.get("OBST", "13,5").split(","))   # static, dynamic obstacles
+    env = gb.BatchedBallEnv(n, w, gb.EnvConfig(num_static=ns, num_dynamic=nd), device="cuda:0", seed=1)
     os.environ.pop("BALLENV_DEBUG_SKIP")
     env.reset()
     acts = env.sample_actions(64, seed=2)
