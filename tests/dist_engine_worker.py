@@ -1,5 +1,5 @@
 """One rank of the multi-rank engine rehearsal (tests/test_gpu_dist.py starts it under
-`python -m torch.distributed.run --nproc-per-node 2`, backend gloo, every rank on cuda:0).
+`python -m torch.distributed.run --nproc-per-node N`, backend gloo, every rank on cuda:0).
 
 Each rank steps its shard() of the global env batch at the defaults (13 + 5 obstacles,
 TimeLimit 1000, autoreset; SURVEY.md §8(e), BASELINE config 4) with caller actions keyed by

@@ -1,8 +1,8 @@
 """Multi-rank engine rehearsal on one GPU (BASELINE config 4's code path).
 
-A fresh child `python -m torch.distributed.run --nproc-per-node 2` (gloo; both ranks on
+A fresh child `python -m torch.distributed.run --nproc-per-node {2, 8}` (gloo; every rank on
 cuda:0; started as a new process, never an exec) runs tests/dist_engine_worker.py: each rank
-steps its shard() of 8192 envs for 120 default-config steps (episode phases set from the global
+steps its shard() of the global batch (8 192, or config 4's 262 144) for 120 / 40 default-config steps (episode phases set from the global
 env id, so goal changes and TimeLimit truncations happen) and all_gathers its stats record.
 This process then runs the whole batch on one rank and checks, bit for bit, that the ranks'
 per-env rewards / dones / obs, their final states, their per-wave stats slots and the gathered
@@ -29,16 +29,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_two_rank_engine_matches_one_rank(gpu, tmp_path):
+@pytest.mark.parametrize("E,T,world", [(8192, 120, 2), (262144, 40, 8)], ids=["2x4096", "config4_8x32768"])
+def test_multi_rank_engine_matches_one_rank(gpu, tmp_path, E, T, world):
+    """2 ranks x 4 096 envs for 120 steps, and BASELINE config 4's split (262 144 envs over 8
+    ranks of 32 768) for 40 steps.  At config 4 the ranks step on step2_kernel and the one-rank
+    run of the whole batch on the one-lane kernel (the batch-size dispatch), so the check is
+    also a cross-kernel one."""
     import gym_ballenv_amd as gb
     from dist_engine_worker import start_lens
-    E, T, W, seed, world = 8192, 120, 10, 0xD157, 2
+    W, seed = 10, 0xD157
     env_vars = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(HERE, "dist_engine_worker.py"), "--out", str(tmp_path), "--envs", str(E),
            "--steps", str(T), "--window", str(W), "--seed", str(seed)]
-    r = subprocess.run(cmd, cwd=ROOT, env=env_vars, capture_output=True, text=True, timeout=100)
+    r = subprocess.run(cmd, cwd=ROOT, env=env_vars, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     ranks = [dict(np.load(tmp_path / f"rank{i}.npz")) for i in range(world)]
 
@@ -56,13 +61,13 @@ def test_two_rank_engine_matches_one_rank(gpu, tmp_path):
     env.status()
     st = {k: v.cpu().numpy() for k, v in env.state_dict().items()}
     slots = env.stats_buf.cpu().numpy()
-    kernel = env.kernel_name("step")
+    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5>" if E <= 98304 else "be_kernel<10, 0, 13, 5>")
 
-    assert done.sum() > E // 10, "episodes must finish and autoreset during the run"
+    assert done.sum() > E * T // 2000, "episodes must finish and autoreset during the run"
     for i, rk in enumerate(ranks):
         off, n = int(rk["off"]), int(rk["n"])
         assert (off, n) == gb.shard(E, i, world)
-        assert str(rk["kernel"]) == kernel
+        assert str(rk["kernel"]) == "step2_kernel<10, 13, 5>"
         sl = slice(off, off + n)
         np.testing.assert_array_equal(rk["reward"], rew[:, sl], err_msg=f"rank {i} reward")
         np.testing.assert_array_equal(rk["done"], done[:, sl], err_msg=f"rank {i} done")
