@@ -2,7 +2,8 @@
 oracle through goal changes and the TimeLimit.
 
 The bench workload (EnvConfig() defaults, caller actions) runs the fixed-shape step kernel
-(step2_kernel<10, 13, 5> at W=10, be_kernel<5, 0, 13, 5> at W=5), the fused be_rollout kernel
+(step2_kernel<10, 13, 5> at W=10 up to 98 304 envs, be_kernel<10, 0, 13, 5> past that,
+be_kernel<5, 0, 13, 5> at W=5), the fused be_rollout kernel
 and the fused be_policy_rollout kernel.
 Each has its own goal re-pick (newGoalList for pairwise-distinct goals, ballenv_env.py:339-353)
 and its own `ep_len mod (goal_change+1)` counter arithmetic, and all of them fold the gym
@@ -25,9 +26,11 @@ pytestmark = pytest.mark.gpu
 SLICE = 2048
 
 
-def fixed_step_kernel(W):
-    """The step kernel pick_kernel selects at the defaults with caller actions."""
-    return "step2_kernel<10, 13, 5>" if W == 10 else f"be_kernel<{W}, 0, 13, 5>"
+def fixed_step_kernel(W, N=0):
+    """The step kernel pick_kernel selects at the defaults with caller actions: step2_kernel at
+    W=10 up to 96 x 4 x CUs envs, the one-lane fixed-shape kernel otherwise."""
+    cut = 96 * 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    return "step2_kernel<10, 13, 5>" if W == 10 and N <= cut else f"be_kernel<{W}, 0, 13, 5>"
 
 
 def _random_lens(N, rng, limit=1000):
@@ -82,7 +85,7 @@ def _check_state(env, st, a, k, msg):
         np.testing.assert_array_equal(got[key], st[key], err_msg=f"{msg}: state[{key}]")
 
 
-@pytest.mark.parametrize("W,N,a", [(10, 65536, 40960), (5, 4096, 1024), (10, 3000, 952)])
+@pytest.mark.parametrize("W,N,a", [(10, 65536, 40960), (5, 4096, 1024), (10, 3000, 952), (10, 262144, 200000)])
 def test_step_kernel_default_episode(gpu, W, N, a):
     """be_step (fixed-shape kernel) at the defaults -- goal change every 51 steps, TimeLimit
     1000, autoreset -- bit-exact against the oracle over 120 steps (>= 2 goal changes per env
@@ -93,7 +96,7 @@ def test_step_kernel_default_episode(gpu, W, N, a):
     rng = np.random.default_rng(W * 7 + N)
     k = min(SLICE, N - a)
     env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, k, seed=0xBA11, rng=rng)
-    assert env.kernel_name("step") == fixed_step_kernel(W)
+    assert env.kernel_name("step") == fixed_step_kernel(W, N)
     acts = env.sample_actions(120, seed=0xBA11)
     n_trunc = n_change = 0
     for t in range(120):
