@@ -16,11 +16,14 @@ import gym_ballenv_amd as gb  # noqa: E402
 from gym_ballenv_amd import _abi  # noqa: E402
 
 
-def make(n, w, dbg):
+def make(n, w, dbg, lpe=""):
     os.environ["BALLENV_DEBUG_SKIP"] = str(dbg)
+    if lpe:
+        os.environ["BALLENV_STEP_LPE"] = lpe
     ns, nd = (int(x) for x in os.environ.get("OBST", "13,5").split(","))   # static, dynamic obstacles
     env = gb.BatchedBallEnv(n, w, gb.EnvConfig(num_static=ns, num_dynamic=nd), device="cuda:0", seed=1)
     os.environ.pop("BALLENV_DEBUG_SKIP")
+    os.environ.pop("BALLENV_STEP_LPE", None)
     env.reset()
     acts = env.sample_actions(64, seed=2)
     return env, acts
@@ -68,14 +71,15 @@ def main():
     masks = [int(m, 0) for m in os.environ.get("MASKS", "0,1,2,6,8,16,24,32,63").split(",")]
     sizes = [int(n) for n in os.environ.get("SIZES", "65536,262144,1048576").split(",")]
     W = int(os.environ.get("W", "10"))
-    envs = {(n, m): make(n, W, m) for n in sizes for m in masks}
+    lpes = os.environ.get("LPES", "").split(",")     # BALLENV_STEP_LPE per context ("" = dispatch)
+    envs = {(n, m, l): make(n, W, m, l) for n in sizes for m in masks for l in lpes}
     res = {k: [] for k in envs}
     for _ in range(5):
         for k, (e, a) in envs.items():
             res[k].append(time_graph(e, a) if os.environ.get("GRAPH") else time_env(e, a))
-    for (n, m), v in sorted(res.items()):
+    for (n, m, l), v in sorted(res.items()):
         v.sort()
-        print(json.dumps({"envs": n, "mask": m, "us_median": round(v[len(v) // 2], 2), "us_min": round(v[0], 2),
+        print(json.dumps({"envs": n, "mask": m, "lpe": l, "kernel": envs[(n, m, l)][0].kernel_name("step"), "us_median": round(v[len(v) // 2], 2), "us_min": round(v[0], 2),
                           "ns_per_env": round(v[len(v) // 2] * 1e3 / n, 3)}))
 
 
