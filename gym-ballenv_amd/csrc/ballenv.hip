@@ -1620,13 +1620,10 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t x) {   // OR with the other
   return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
 }
 
-// L = 4 (four lanes per env) exists only in diagnostics builds (-DBE_STEP4, BALLENV_STEP_LPE=4):
-// a timing proxy without the episode-statistics fold, whose 32-env slots would span two waves.
-template <int WT, int NSC, int NDC, int L = 2>
-__global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
+template <int WT, int NSC, int NDC>
+__global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   constexpr int CT = S2_CT;
-  static_assert(L == 2 || L == 4, "two or four lanes per env");
-  constexpr int EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
+  constexpr int L = 2, EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
   constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;   // obstacle slots per lane
   constexpr int KR = Geo<WT>::K, F = Geo<WT>::F, NW = Geo<WT>::NW;
   constexpr int NQ = F / 8, HQ = (NQ + 1) / 2;                     // uint2 words per row / per lane
@@ -1640,8 +1637,8 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
 
   DIAG(0);
   if (DBG(DBG_EXIT_ENTRY)) return;
-  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
-  const int blk0 = (int)blockIdx.x * EPB, i = blk0 + tid / L, e0 = blk0 + w * EPW;
+  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & 1;
+  const int blk0 = (int)blockIdx.x * EPB, i = blk0 + (tid >> 1), e0 = blk0 + w * EPW;
   uint8_t* stage_blk = smem + (size_t)(SS + SD + 1) * CT * 4;   // [EPB envs][F]
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
@@ -1675,7 +1672,7 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
   double ret = ld_s(p.ep_return, ic);
   // the wave's stats slot (one per 32 envs), read now: a wave with a finished env updates it at
   // the very end, and a dependent load there would lengthen exactly the waves that reset
-  double* const slot = (L == 2 && p.stats) ? p.stats + ((size_t)blockIdx.x * NWAVE + w) * 8 : nullptr;
+  double* const slot = p.stats ? p.stats + ((size_t)blockIdx.x * NWAVE + w) * 8 : nullptr;
   double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sp2 = sp0;
   if (slot && lane == 0 && e0 < N) {
     sp0 = reinterpret_cast<const double2*>(slot)[0];
@@ -1739,9 +1736,7 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
     const int k = L * j + h;
     const bool real = k < NDC;
     int ox = px(dp[j]), oy = py(dp[j]);
-    uint32_t f;
-    if constexpr (L == 2) f = h ? pick_field(b0, min(L * j + 1, 4)) : pick_field(b0, L * j);
-    else f = pick_field(b0, min(L * j + h, 4));
+    const uint32_t f = h ? pick_field(b0, min(L * j + 1, 4)) : pick_field(b0, L * j);
     uint32_t fl = 0u;
     ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[min(k, NDC - 1)], change, f, fl);
     st_flags |= real ? fl : 0u;
@@ -1751,8 +1746,8 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
   DIAG(11);
 #pragma unroll
   for (int j = 0; j < SS; ++j) obstacle_pk(so[j], L * j + h < NSC, hs);
-  hs = group_or<L>((uint32_t)hs) != 0u;
-  hd = group_or<L>((uint32_t)hd) != 0u;
+  hs = pair_or((uint32_t)hs) != 0u;
+  hd = pair_or((uint32_t)hd) != 0u;
   DIAG(10);
 
   // ---- distance, reward, done (ballenv_env.py:268-286, 200-229), on both lanes
@@ -1765,7 +1760,7 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
   const bool trunc = p.time_limit > 0 && len >= p.time_limit;
   const bool done = env_done || trunc;
   const bool do_reset = valid && done && p.autoreset;
-  if (valid && L == 2) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
+  if (valid) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
     double* pd = h ? p.ep_return : p.reward;
     st_wt(pd + i, h ? ret : reward);
     int32_t* pi = h ? p.ep_len : p.agent;
@@ -1777,19 +1772,6 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
       if (!h && p.final_return) st_wt(p.final_return + i, ret);
       if (h && p.final_len) st_wt(p.final_len + i, len);
     }
-  } else if (valid) {   // four lanes: reward + done | ep_return + truncated | agent + prev_dist | ep_len
-    double* pd = (h & 1) ? p.ep_return : (h ? p.prev_dist : p.reward);
-    if (h != 3) st_wt(pd + i, h == 1 ? ret : (h ? dist : reward));
-    if (h == 2) st_wt(p.agent + i, pk(ax, ay));
-    if (h == 3) st_wt(p.ep_len + i, len);
-    uint8_t* pb = h ? p.truncated : p.done;
-    if (pb && h < 2) st_wt(pb + i, (uint8_t)(h ? (trunc && !env_done) : done));
-    if (done) {
-      if (h == 1 && p.final_return) st_wt(p.final_return + i, ret);
-      if (h == 3 && p.final_len) st_wt(p.final_len + i, len);
-    }
-  }
-  if (valid) {
     // (stored after done is known: measured faster than storing inside the obstacle loop)
 #pragma unroll
     for (int j = 0; j < SD; ++j) {
@@ -1818,7 +1800,7 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
     uint32_t rows[KR], flat[NW];
     raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
 #pragma unroll
-    for (int k = 0; k < KR; ++k) rows[k] = group_or<L>(rows[k]);
+    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k]);
     flatten<WT>(rows, flat);
     if (!h) write_row_global<WT>(p.terminal_obs + (int64_t)i * F, flat, quadrant(ax, ay, gx, gy));
   }
@@ -1859,25 +1841,9 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
     uint32_t rows[KR], flat[NW];
     raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
 #pragma unroll
-    for (int k = 0; k < KR; ++k) rows[k] = group_or<L>(rows[k] | xrows[k]);
+    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k] | xrows[k]);
     flatten<WT>(rows, flat);
     const int quad = quadrant(ax, ay, gx, gy);
-    if constexpr (L == 4) {
-      // lane h writes row words [q0, q1) = {0,4,7,10,13}[h..h+1]: word q holds cells 8q-4 .. 8q+3
-      const int q0 = h == 0 ? 0 : 3 * h + 1, nq = h == 0 ? 4 : 3;
-      const int sb = 8 * q0 - 4;                      // first cell of this lane's words (-4: quadrant)
-      const uint32_t c = h == 0 ? flat[0] << 4
-                       : h == 1 ? (flat[0] >> 28) | (flat[1] << 4)
-                       : h == 2 ? (flat[1] >> 20) | (flat[2] << 12) : (flat[2] >> 12) | (flat[3] << 20);
-      (void)sb;
-      auto word4 = [&](int jj) -> uint32_t { return (((c >> (4 * jj)) & 0xFu) * 0x00204081u) & 0x01010101u; };
-      uint2* dst = reinterpret_cast<uint2*>(stage + (lane >> 2) * F) + q0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t w0 = (q == 0 && h == 0) ? 1u << (8 * quad) : word4(2 * q);
-        if (q < nq) dst[q] = make_uint2(w0, word4(2 * q + 1));
-      }
-    } else {
     // uint2 word q of this lane is row word 2(q + 7h) .. +1: word j >= 1 expands cells
     // 4(j-1) .. 4(j-1)+3.  c holds this lane's cells from bit 0: lane 0 cells -4.. (its word 0
     // is the quadrant one-hot), lane 1 cells 52..
@@ -1893,7 +1859,6 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
     for (int q = 0; q < HQ; ++q) {
       const uint32_t w0 = q == 0 ? (h ? word(0) : 1u << (8 * quad)) : word(2 * q);
       if (q < NQ - HQ || !h) dst[q] = make_uint2(w0, word(2 * q + 1));
-    }
     }
   }
   DIAG(4);
@@ -1912,7 +1877,7 @@ __global__ __launch_bounds__(S2_CT, L) void step2_kernel(KParams p) {
   // the episode statistics fold after the obs stores are issued: off the path to the last store
   // (6.55 -> 6.45 us; a reset leaves this lane's ret / len registers as the finished episode's)
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
-  if (L == 2 && slot && !DBG(DBG_NO_STATS)) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
+  if (slot && !DBG(DBG_NO_STATS)) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
   if (slot && lane == 0 && ws.n > 0.0) {
     reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
     reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
@@ -2382,14 +2347,14 @@ struct Launch { KFn fn; int epb; int lds; char name[48]; int threads = BLOCK_THR
 #endif
 constexpr int FIX_NS = BE_FIX_NS, FIX_ND = BE_FIX_ND;
 
-Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lanes = 1) {
+Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe2_ok = false) {
   int W = c.window;
   const int F = 4 + W * W, nobs = c.num_static + c.num_dynamic;
   Launch L{nullptr, 0, 0, {0}};
   bool staged = true;
   const bool fixed = fixed_ok && mode == MODE_STEP && c.num_static == FIX_NS && c.num_dynamic == FIX_ND &&
                      c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
-  if (fixed && lanes == 2 && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
+  if (fixed && lpe2_ok && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
     // two lanes per env (step2_kernel): 32 envs per wave, 128 per block
     L.fn = step2_kernel<10, FIX_NS, FIX_ND>;
     L.epb = S2_CT / 2;
@@ -2399,17 +2364,6 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lane
     snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d>", FIX_NS, FIX_ND);
     return L;
   }
-#ifdef BE_STEP4
-  if (fixed && lanes == 4 && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
-    L.fn = step2_kernel<10, FIX_NS, FIX_ND, 4>;
-    L.epb = S2_CT / 4;
-    L.threads = S2_CT;
-    constexpr int SLOTS = (FIX_NS + 3) / 4 + (FIX_ND + 3) / 4 + 1;
-    L.lds = SLOTS * S2_CT * 4 + L.epb * F;
-    snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d, 4>", FIX_NS, FIX_ND);
-    return L;
-  }
-#endif
   if (fixed && W == 10) { L.fn = be_kernel<10, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
   else if (fixed && W == 5) { L.fn = be_kernel<5, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
   switch (W) {
@@ -2474,7 +2428,7 @@ struct be_ctx {
   bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
-  int step_lanes;      // lanes per env of the W=10 fixed step kernel: 1 (be_kernel) or 2 (step2_kernel)
+  bool step_lpe1;      // the one-lane-per-env fixed step kernel instead of step2_kernel (see below)
   char err[512];
 };
 
@@ -2607,7 +2561,7 @@ const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
   const bool fixed_ok = !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals;
   Launch L{nullptr, 0, 0, {0}};
   switch (entry) {
-    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, ctx->step_lanes); break;
+    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, !ctx->step_lpe1); break;
     case BE_ENTRY_STEP_SAMPLED: L = pick_kernel(ctx->cfg, MODE_STEP, false); break;
     case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok); break;
     case BE_ENTRY_RESET: L = pick_kernel(ctx->cfg, MODE_RESET, false); break;
@@ -2675,9 +2629,9 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
      // BALLENV_STEP_LPE=1 / 2 forces one or two lanes (A/B).
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
-    ctx->step_lanes = (int64_t)cfg->num_envs > (int64_t)96 * 4 * cus ? 1 : 2;
+    ctx->step_lpe1 = (int64_t)cfg->num_envs > (int64_t)96 * 4 * cus;
   }
-  if (const char* l = getenv("BALLENV_STEP_LPE")) ctx->step_lanes = atoi(l) == 1 ? 1 : atoi(l) == 4 ? 4 : 2;
+  if (const char* l = getenv("BALLENV_STEP_LPE")) ctx->step_lpe1 = atoi(l) == 1;
   Tables& t = ctx->tables;
   memset(&t, 0, sizeof t);
   for (int k = 0; k < cfg->num_dynamic; ++k) t.speed[k] = cfg->obstacle_speed[k];
@@ -2761,7 +2715,7 @@ static int launch(be_ctx* ctx, int mode, KParams& a, void* stream, int32_t steps
   int cur = -1;
   HIP_TRY(ctx, hipGetDevice(&cur));
   if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, ctx->step_lanes);
+  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, !ctx->step_lpe1);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)L.threads);
   for (int32_t s = 0; s < steps; ++s) {
