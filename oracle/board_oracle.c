@@ -10,7 +10,8 @@
  *   featureExtractor.py featureExtractor :247-265 (calcDistanceFromGoal :132-144,
  *                       relativeGoalPos :146-166, densityFeatures :91-112,
  *                       speedOrientationFeatures :115-130, socialForcesFeatures :170-193)
- * Draws come from a tape (the reference's ranf/randint values in call order).
+ * Draws come from a tape (the reference's ranf/randint values in call order), or in
+ * orc_board_reset_philox from the engine's own Philox layout (its own draws, not the reference's).
  */
 #include <math.h>
 
@@ -89,6 +90,87 @@ int orc_board_reset(const be_board_config* c, const be_board_state* st, const do
     st->agent[2 * i] = ax; st->agent[2 * i + 1] = ay; st->goal[2 * i] = gx; st->goal[2 * i + 1] = gy;
     st->dist[i] = d0; st->total_dist[i] = bdist(ax, ay, gx, gy); st->ep_return[i] = 0.0; st->ep_len[i] = 0;
     st->episode[i] += 1u;
+    if (features) board_features(c, st, i, features + (int64_t)i * 20);
+  }
+  return status;
+}
+
+/* createBoard.reset (:460-513) in Philox mode: the draw layout of board.hip's
+ * wave_board_resets, restated sequentially.  Counter (global env id, new episode, 0,
+ * 6 << 24 | sub): sub 0 = the goal (gx from words x,y, gy from z,w), 1<<20 | r = agent attempt r,
+ * 2<<20 | k<<12 | a = static k attempt a; ranf = 53 bits from two words, randint = multiply-shift
+ * of one word.  The rejection loops take the first accepted attempt in attempt order; the GPU
+ * checks them in passes (64 agent attempts, 64/ns attempts per static) and, past the limit,
+ * gives up with the pass's last agent attempt / the static's first attempt of the pass. */
+void orc_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]);
+#define BOARD_PURPOSE 6u
+#define BOARD_LIMIT 4096
+static void board_block(const be_board_config* c, uint32_t gid, uint32_t ep, uint32_t sub, uint32_t o[4]) {
+  const uint32_t ctr[4] = {gid, ep, 0u, (BOARD_PURPOSE << 24) | (sub & 0xFFFFFFu)};
+  orc_philox4x32_10(ctr, (uint32_t)c->seed, (uint32_t)(c->seed >> 32), o);
+}
+static double ranf2(uint32_t w0, uint32_t w1) {
+  return ((double)(w0 >> 5) * 67108864.0 + (double)(w1 >> 6)) * (1.0 / 9007199254740992.0);
+}
+static int32_t umulhi_range(uint32_t w, int32_t lo, int32_t hi) {
+  return lo + (int32_t)(((uint64_t)w * (uint64_t)(uint32_t)(hi - lo)) >> 32);
+}
+
+int orc_board_reset_philox(const be_board_config* c, const be_board_state* st, const uint8_t* mask, float* features) {
+  const int32_t N = c->num_envs, ns = c->num_static;
+  const int per = ns > 0 ? 64 / ns : 64;
+  const double rc = c->static_radius + c->agent_radius;
+  int status = 0;
+  for (int32_t i = 0; i < N; ++i) {
+    if (mask && !mask[i]) continue;
+    const uint32_t gid = (uint32_t)(c->env_offset + i), ep = st->episode[i] + 1u;
+    uint32_t o[4];
+    board_block(c, gid, ep, 0u, o);                                    /* goal (:462-463) */
+    const double gx = (double)(c->screen_width - c->strip_goal_x) + ranf2(o[0], o[1]) * (double)c->strip_goal_x;
+    const double gy = (double)(c->screen_height - c->strip_goal_y) + ranf2(o[2], o[3]) * (double)c->strip_goal_y;
+    double ax = 0, ay = 0, d0 = 0;
+    for (int r0 = 0;; r0 += 64) {                                      /* agent (:464-481) */
+      int found = -1;
+      double cx[64], cy[64];
+      for (int l = 0; l < 64; ++l) {
+        board_block(c, gid, ep, (1u << 20) | (uint32_t)(r0 + l), o);
+        cx[l] = ranf2(o[0], o[1]) * (double)c->strip_agent_x;
+        cy[l] = ranf2(o[2], o[3]) * (double)c->strip_agent_y;
+        const double dc = bdist(gx, gy, cx[l], cy[l]);
+        if (r0 == 0 && l == 0) d0 = dc;                                 /* state[2]: the first distance */
+        if (found < 0 && !(dc < c->min_spawn_dist)) found = l;
+      }
+      if (found >= 0 || r0 + 64 > BOARD_LIMIT) {
+        if (found < 0) { status |= BE_STATUS_REJECTION_LIMIT; found = 63; }
+        ax = cx[found]; ay = cy[found];
+        break;
+      }
+    }
+    for (int32_t k = 0; k < ns; ++k) {                                 /* statics (:489-498) */
+      int32_t ox = 0, oy = 0;
+      for (int a0 = 0;; a0 += per) {
+        int found = 0;
+        int32_t fx = 0, fy = 0;
+        for (int a = a0; a < a0 + per && !found; ++a) {
+          board_block(c, gid, ep, (2u << 20) | ((uint32_t)k << 12) | (uint32_t)a, o);
+          fx = umulhi_range(o[0], c->strip_obs_x, c->screen_width - c->strip_obs_x);
+          fy = umulhi_range(o[1], c->strip_obs_y, c->screen_height - c->strip_obs_y);
+          found = bdist(fx, fy, ax, ay) - c->spawn_thresh_agent > rc && bdist(fx, fy, gx, gy) - c->spawn_thresh_goal > rc;
+        }
+        if (found) { ox = fx; oy = fy; break; }
+        if (a0 + per > BOARD_LIMIT) {
+          status |= BE_STATUS_REJECTION_LIMIT;
+          board_block(c, gid, ep, (2u << 20) | ((uint32_t)k << 12) | (uint32_t)a0, o);
+          ox = umulhi_range(o[0], c->strip_obs_x, c->screen_width - c->strip_obs_x);
+          oy = umulhi_range(o[1], c->strip_obs_y, c->screen_height - c->strip_obs_y);
+          break;
+        }
+      }
+      st->static_obs[(int64_t)k * N + i] = (int32_t)(((uint32_t)(uint16_t)ox) | ((uint32_t)(uint16_t)oy << 16));
+    }
+    st->agent[2 * i] = ax; st->agent[2 * i + 1] = ay; st->goal[2 * i] = gx; st->goal[2 * i + 1] = gy;
+    st->dist[i] = d0; st->total_dist[i] = bdist(ax, ay, gx, gy); st->ep_return[i] = 0.0; st->ep_len[i] = 0;
+    st->episode[i] = ep;
     if (features) board_features(c, st, i, features + (int64_t)i * 20);
   }
   return status;

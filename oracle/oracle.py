@@ -46,6 +46,7 @@ def lib():
         L.orc_observe_blocks.argtypes = [vp, vp, vp]
         L.orc_board_reset.argtypes = [vp, vp, vp, i32, vp]
         L.orc_board_step.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.orc_board_reset_philox.argtypes = [vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -158,6 +159,14 @@ def board_reset(cfg, st, tape):
     tape = np.ascontiguousarray(tape, dtype=np.float64)
     f = np.zeros((cfg.num_envs, 20), np.float32)
     s = lib().orc_board_reset(C.byref(cfg), C.byref(_board_struct(st)), _p(tape), tape.shape[0], _p(f))
+    return s, f
+
+
+def board_reset_philox(cfg, st, mask=None):
+    """Philox-mode reset of the (masked) envs in the engine's draw layout; returns (status, features)."""
+    m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+    f = np.zeros((cfg.num_envs, 20), np.float32)
+    s = lib().orc_board_reset_philox(C.byref(cfg), C.byref(_board_struct(st)), _p(m), _p(f))
     return s, f
 
 

@@ -2,7 +2,8 @@
  * AddressSanitizer + UndefinedBehaviorSanitizer on the host (`make -C oracle sanitize`).
  * Covers tape and Philox resets, caller actions / deltas / sampled actions, W = 1, 5, 10, 21,
  * the default and a custom obstacle config, mass TimeLimit truncation with terminal obs and
- * stats, prep_state2 blocks, and the createBoard profile -- every public orc_* entry point. */
+ * stats, prep_state2 blocks, and the createBoard profile (tape and Philox resets) -- every public
+ * orc_* entry point. */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -24,6 +25,7 @@ int orc_board_reset(const be_board_config* c, const be_board_state* st, const do
                     float* features);
 int orc_board_step(const be_board_config* c, const be_board_state* st, const uint8_t* actions, const double* deltas,
                    double* reward, uint8_t* done, float* features);
+int orc_board_reset_philox(const be_board_config* c, const be_board_state* st, const uint8_t* mask, float* features);
 
 static uint64_t rng = 0x9E3779B97F4A7C15ull;
 static uint32_t rnd(void) { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return (uint32_t)(rng >> 16); }
@@ -131,6 +133,7 @@ static int run_board(int32_t N, int32_t ns, int steps) {
   for (int t = 0; t < steps; ++t) {
     for (int32_t i = 0; i < N; ++i) { a[i] = (uint8_t)(rnd() % 4); d[2 * i] = (rnd() % 7) - 3.0; d[2 * i + 1] = (rnd() % 7) - 3.0; }
     orc_board_step(&c, &st, (t & 1) ? a : NULL, (t & 1) ? NULL : d, rew, done, feats);
+    if (t % 5 == 4) status |= orc_board_reset_philox(&c, &st, done, feats);   /* Philox autoreset of the done envs */
   }
   double s = 0;
   for (int64_t k = 0; k < (int64_t)N * 20; ++k) s += feats[k];

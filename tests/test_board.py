@@ -181,3 +181,49 @@ def test_gpu_board_rollout_matches_steps(gpu, use_deltas):
     b.status()
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ns", [6, 8, 0])
+def test_gpu_board_philox_resets_vs_oracle(gpu, ns):
+    """Philox-mode resets (be_board_reset without a tape, and the autoreset inside be_board_step)
+    bit-exact against the oracle's sequential restatement of the engine's draw layout
+    (orc_board_reset_philox): a full reset, a masked reset, then 40 random moves with autoreset.
+    The draws are the engine's own (Philox), so this pins the layout, not the reference."""
+    N, seed, off = 5000, 0x5EED, 12345
+    b = make_board(gpu, N, ns, seed=seed, env_offset=off, autoreset=True)
+    cfg = b.cfg
+    st = oracle.board_new_state(cfg)
+    rng = np.random.default_rng(ns)
+
+    def check(msg):
+        for k in b.STATE_KEYS:
+            got = getattr(b, k).cpu().numpy()
+            want = st[k].view(np.int32) if k == "episode" else st[k]
+            np.testing.assert_array_equal(got, want, err_msg=f"{msg}: {k}")
+
+    f = b.reset()
+    s, wf = oracle.board_reset_philox(cfg, st)
+    assert s == 0
+    check("reset")
+    check_features(f.cpu().numpy(), wf, "reset")
+    mask = rng.random(N) < 0.3
+    f = b.reset(mask=torch.from_numpy(mask))
+    s, wf2 = oracle.board_reset_philox(cfg, st, mask=mask)
+    check("masked reset")
+    check_features(f.cpu().numpy()[mask], wf2[mask], "masked reset")
+    n_done = 0
+    for t in range(40):   # float mouse moves (sigma 4): hits and goals within a few dozen steps
+        dl = rng.normal(0, 4, (N, 2))
+        f, r, d, _ = b.step(deltas=torch.from_numpy(dl))
+        wr, wd, wf = oracle.board_step(cfg, st, deltas=dl)
+        dm = wd.astype(bool)
+        _, wfr = oracle.board_reset_philox(cfg, st, mask=dm)
+        np.testing.assert_array_equal(r.cpu().numpy(), wr, err_msg=f"reward t={t}")
+        np.testing.assert_array_equal(d.cpu().numpy(), dm, err_msg=f"done t={t}")
+        check(f"t={t}")
+        check_features(f.cpu().numpy(), np.where(dm[:, None], wfr, wf), f"t={t}")
+        n_done += int(dm.sum())
+    assert n_done > N // 50, n_done
+    b.status()
+    b.close()
