@@ -200,49 +200,98 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-template <int MAXS>
+// P envs per pass (P = 1, 2, 4): the wave's lanes split into P slots of LS = 64 / P lanes, slot s
+// resetting the pass's s-th finished env.  A slot checks its attempts in order, LS agent attempts
+// or LS / ns attempts per static at a time, so every env gets the first accepted attempt of its
+// rejection loop whatever P is; the give-up points (BOARD_REJECT_LIMIT) are those of the 64-lane
+// passes (64 agent attempts, 64 / ns per static), which oracle/board_oracle.c restates.  Needs
+// ns <= LS.  The slot's lanes end up holding its env's new state; the env's own lane (the owner)
+// picks it up with uniform readlanes.
+template <int MAXS, int P>
 __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32_t gid, uint32_t episode_new,
                                   double& ax, double& ay, double& gx, double& gy, double& d0, double& total,
                                   int32_t (&so)[MAXS]) {
-  const int lane = (int)(threadIdx.x & 63);
+  constexpr int LS = 64 / P;
+  constexpr unsigned long long SMASK = LS == 64 ? ~0ull : (1ull << LS) - 1;
+  constexpr int AG_END = (BOARD_REJECT_LIMIT / 64 + 1) * 64;   // the 64-lane agent passes give up after this
+  const int lane = (int)(threadIdx.x & 63), slot = lane / LS, sl = lane - slot * LS;
   const int ns = p.ns;
-  const int per = ns > 0 ? 64 / ns : 64;   // static attempts per pass
+  const int per64 = ns > 0 ? 64 / ns : 64;                      // 64-lane static pass length
+  const int st_g0 = BOARD_REJECT_LIMIT / per64 * per64;         // first 64-lane pass a0 with a0 + per64 > LIMIT
+  const int st_end = st_g0 + per64;                             // attempts past this are never taken
+  const int per = ns > 0 ? LS / ns : LS;                        // this slot's attempts per static per pass
+  const int k_l = ns > 0 ? sl % ns : 0, a_l = ns > 0 ? sl / ns : 0;
+  unsigned long long kbase = 0;                                 // lanes (a, k = 0) of a slot
+  for (int a = 0; a < per; ++a) kbase |= 1ull << (a * ns);
   while (m) {
-    const int l = __ffsll((long long)m) - 1;
-    m &= m - 1;
-    const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)gid, l);
-    const uint32_t ep = (uint32_t)__builtin_amdgcn_readlane((int)episode_new, l);
-    // goal (every lane: same block), agent attempts r0 + lane (ballenv_pygame.py:462-470)
+    int ls[P], n = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < P; ++s2) {   // the next (up to) P finished lanes, in lane order
+      ls[s2] = m ? __ffsll((long long)m) - 1 : 0;
+      n += m ? 1 : 0;
+      m &= m - 1;
+    }
+    uint32_t u = 0, ep = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < P; ++s2) {
+      const uint32_t u2 = (uint32_t)__builtin_amdgcn_readlane((int)gid, ls[s2]);
+      const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)episode_new, ls[s2]);
+      u = slot == s2 ? u2 : u; ep = slot == s2 ? e2 : ep;
+    }
+    const bool act = slot < n;
+    // goal (ballenv_pygame.py:462-463), on every lane of the slot
     const u4 bg = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, 0u), p.seed);
     const double rgx = (double)(p.W - p.sgx) + ranf2(bg.x, bg.y) * (double)p.sgx;
     const double rgy = (double)(p.H - p.sgy) + ranf2(bg.z, bg.w) * (double)p.sgy;
+    // agent attempts r0 + sl (:464-481)
     double rax = 0.0, ray = 0.0, rd0 = 0.0;
-    for (int r0 = 0;; r0 += 64) {
-      const u4 ba = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (1u << 20) | (uint32_t)(r0 + lane)), p.seed);
+    unsigned open = (1u << n) - 1u;
+    for (int r0 = 0; open; r0 += LS) {
+      const u4 ba = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (1u << 20) | (uint32_t)(r0 + sl)), p.seed);
       const double cx = ranf2(ba.x, ba.y) * (double)p.sax, cy = ranf2(ba.z, ba.w) * (double)p.say;
       const double dc = dist2(rgx, rgy, cx, cy);
-      if (r0 == 0) rd0 = readlane_f64(dc, 0);                     // state[2]: the first distance
-      const unsigned long long ok = __ballot(!(dc < p.min_spawn));
-      if (ok || r0 + 64 > BOARD_REJECT_LIMIT) {
-        if (!ok) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
-        const int q = ok ? __ffsll((long long)ok) - 1 : 63;
-        rax = readlane_f64(cx, q); ray = readlane_f64(cy, q);
-        break;
+      if (r0 == 0) {
+#pragma unroll
+        for (int s2 = 0; s2 < P; ++s2) {   // state[2]: the first attempt's distance
+          const double d = readlane_f64(dc, s2 * LS);
+          rd0 = slot == s2 ? d : rd0;
+        }
+      }
+      const unsigned long long ok = __ballot(act && !(dc < p.min_spawn));
+      const bool last = r0 + LS >= AG_END;
+#pragma unroll
+      for (int s2 = 0; s2 < P; ++s2) {
+        if (!((open >> s2) & 1u)) continue;
+        const unsigned long long hit = (ok >> (s2 * LS)) & SMASK;
+        if (hit || last) {
+          if (!hit && lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+          const int q = s2 * LS + (hit ? __ffsll((long long)hit) - 1 : LS - 1);
+          const double x = readlane_f64(cx, q), y = readlane_f64(cy, q);
+          rax = slot == s2 ? x : rax; ray = slot == s2 ? y : ray;
+          open &= ~(1u << s2);
+        }
       }
     }
-    // statics (:489-498): lane = a * ns + k, the first accepted attempt of each k
-    const int k_l = ns > 0 ? lane % ns : 0, a_l = ns > 0 ? lane / ns : 0;
-    const bool in_pass = ns > 0 && a_l < per;
-    int32_t cand = 0;
-    unsigned long long need = ns > 0 ? ((ns >= 64 ? ~0ull : (1ull << ns) - 1)) : 0ull;   // statics still open
+    // statics (:489-498): slot lane a * ns + k draws attempt a0 + a of static k
+    unsigned long long need[P];
+#pragma unroll
+    for (int s2 = 0; s2 < P; ++s2) need[s2] = s2 < n && ns > 0 ? (ns >= 64 ? ~0ull : (1ull << ns) - 1) : 0ull;
     int32_t got[MAXS];
 #pragma unroll
     for (int k = 0; k < MAXS; ++k) got[k] = 0;
-    for (int a0 = 0; need; a0 += per) {
+    for (int a0 = 0;; a0 += per) {
+      unsigned long long any = 0;
+#pragma unroll
+      for (int s2 = 0; s2 < P; ++s2) any |= need[s2];
+      if (!any) break;
+      unsigned long long mine = 0;
+#pragma unroll
+      for (int s2 = 0; s2 < P; ++s2) mine = slot == s2 ? need[s2] : mine;
+      const int a = a0 + a_l;
       bool ok = false;
-      if (in_pass) {
-        const u4 bo = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (2u << 20) | ((uint32_t)k_l << 12) | (uint32_t)(a0 + a_l)),
-                             p.seed);
+      int32_t cand = 0;
+      if (act && ns > 0 && a_l < per && a < st_end && ((mine >> k_l) & 1ull)) {
+        const u4 bo = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (2u << 20) | ((uint32_t)k_l << 12) | (uint32_t)a), p.seed);
         const int ox = p.sox + (int)__umulhi(bo.x, (uint32_t)(p.W - 2 * p.sox));
         const int oy = p.soy + (int)__umulhi(bo.y, (uint32_t)(p.H - 2 * p.soy));
         ok = dist2((double)ox, (double)oy, rax, ray) - p.thr_agent > p.r_collide &&
@@ -250,26 +299,45 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
         cand = (int32_t)(((uint32_t)ox & 0xFFFFu) | ((uint32_t)oy << 16));
       }
       const unsigned long long okm = __ballot(ok);
-      const bool give_up = a0 + per > BOARD_REJECT_LIMIT;
+      const bool last = a0 + per >= st_end;
 #pragma unroll
-      for (int k = 0; k < MAXS; ++k) {
-        if (k >= ns || !((need >> k) & 1ull)) continue;
-        // lanes of static k: k, k + ns, k + 2 ns, ... (attempt order)
-        unsigned long long km = 0;
-        for (int a = 0; a < per; ++a) km |= 1ull << (a * ns + k);
-        const unsigned long long hit = okm & km;
-        if (hit || give_up) {
-          if (!hit && lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
-          got[k] = __builtin_amdgcn_readlane(cand, hit ? __ffsll((long long)hit) - 1 : k);
-          need &= ~(1ull << k);
+      for (int s2 = 0; s2 < P; ++s2) {
+#pragma unroll
+        for (int k = 0; k < MAXS; ++k) {
+          if (k >= ns || !((need[s2] >> k) & 1ull)) continue;
+          const unsigned long long hit = okm & ((kbase << k) << (s2 * LS));
+          if (hit || last) {
+            int32_t v;
+            if (hit) {
+              v = __builtin_amdgcn_readlane(cand, __ffsll((long long)hit) - 1);
+            } else {   // rejection limit: the static's first attempt of the last 64-lane pass
+              if (lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+              const u4 bo = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (2u << 20) | ((uint32_t)k << 12) | (uint32_t)st_g0),
+                                   p.seed);
+              const int ox = p.sox + (int)__umulhi(bo.x, (uint32_t)(p.W - 2 * p.sox));
+              const int oy = p.soy + (int)__umulhi(bo.y, (uint32_t)(p.H - 2 * p.soy));
+              v = __builtin_amdgcn_readlane((int)(((uint32_t)ox & 0xFFFFu) | ((uint32_t)oy << 16)), s2 * LS);
+            }
+            got[k] = slot == s2 ? v : got[k];
+            need[s2] &= ~(1ull << k);
+          }
         }
       }
     }
-    if (lane == l) {
-      gx = rgx; gy = rgy; ax = rax; ay = ray; d0 = rd0;
-      total = dist2(rax, ray, rgx, rgy);                           // total_distance
+    // the owners pick up their slot's state
 #pragma unroll
-      for (int k = 0; k < MAXS; ++k) so[k] = got[k];
+    for (int s2 = 0; s2 < P; ++s2) {
+      if (s2 >= n) break;
+      const int src = s2 * LS;
+      const double sgx = readlane_f64(rgx, src), sgy = readlane_f64(rgy, src);
+      const double sax = readlane_f64(rax, src), say = readlane_f64(ray, src), sd0 = readlane_f64(rd0, src);
+      const bool own = lane == ls[s2];
+      if (own) { gx = sgx; gy = sgy; ax = sax; ay = say; d0 = sd0; total = dist2(sax, say, sgx, sgy); }   // total_distance
+#pragma unroll
+      for (int k = 0; k < MAXS; ++k) {
+        const int32_t v = __builtin_amdgcn_readlane(got[k], src);
+        if (own) so[k] = v;
+      }
     }
   }
 }
@@ -343,7 +411,17 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       if (do_reset) reset_env(p, i, episode + 1u, ax, ay, gx, gy, dist, total, so);
     } else {
       const unsigned long long m = __ballot(do_reset);
-      if (m) wave_board_resets<MAXS>(p, m, (uint32_t)p.gid0 + (uint32_t)i, episode + 1u, ax, ay, gx, gy, dist, total, so);
+      if (m) {   // several finished envs: 2 or 4 per pass (ns must fit a slot: ns <= 64 / P)
+        const int nf = __popcll(m);
+        const uint32_t g = (uint32_t)p.gid0 + (uint32_t)i;
+        if constexpr (MAXS > 16) {   // (ns > 16 never fits two slots)
+          wave_board_resets<MAXS, 1>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+        } else {
+          if (nf == 1) wave_board_resets<MAXS, 1>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+          else if (nf == 2 || p.ns > 8) wave_board_resets<MAXS, 2>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+          else wave_board_resets<MAXS, 4>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+        }
+      }
     }
     if (do_reset) {
       ++episode;
