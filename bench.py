@@ -369,6 +369,38 @@ def rollout_leg(args, gb, dev, rank, world, stream):
     return res
 
 
+def committed_pmc(fname, kernel_sub, units):
+    """A committed tools/pmc_report.py profile, if it was taken on this kernel at this many units
+    per dispatch (else None)."""
+    path = os.path.join(ROOT, "profiles", fname)
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    if d.get("units_per_dispatch") != units or kernel_sub not in (d.get("kernel") or ""):
+        return None
+    d["source"] = "committed profile " + os.path.relpath(path, ROOT)
+    return d
+
+
+def board_roofline(B, N, us, pmc):
+    """HBM roofline of a createBoard kernel plus its committed counters: f64-VALU work, not HBM."""
+    ach = B * N / (us * 1e-6) / 1e9
+    r = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+         "traffic": None,
+         "limiter": "neither roofline: f64 VALU (featureExtractor: 7 correctly rounded sqrt, 6 exp, acos, hypot "
+                    "per env-step) at one wave per SIMD"}
+    if pmc:
+        ws = pmc["wave_cycle_split"]
+        r.update({"traffic": pmc["hbm_bytes_per_dispatch"], "traffic_per_env_step": pmc["hbm_bytes_per_unit"],
+                  "valu_insts_per_wave": pmc["per_wave"]["SQ_INSTS_VALU"],
+                  "wave_cycle_split": ws, "pmc_source": pmc["source"],
+                  "limiter": "neither roofline, one wave per SIMD: a wave issues VALU %.0f %% and waits (memory, "
+                             "dependencies) %.0f %% of its cycles; the work is f64 (featureExtractor: 7 correctly "
+                             "rounded sqrt, 6 exp, acos, hypot per env-step)" % (100 * ws["SQ_ACTIVE_INST_VALU"],
+                                                                                  100 * ws["SQ_WAIT_ANY"])})
+    return r
+
+
 def board_leg(args, gb, dev, rank, world, stream):
     """createBoard profile (ballenv_pygame.py:314-706 + featureExtractor): step + 20 features
     for every env, random actionArray moves, 6 static obstacles, autoreset, graph replay."""
@@ -397,6 +429,7 @@ def board_leg(args, gb, dev, rank, world, stream):
                        "random actionArray moves, autoreset, hipGraph replay",
            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
            "kernel_us_mean": ms * 1e3, "bytes_per_env_step": B, "achieved_GBs": B * N / (ms * 1e-3) / 1e9}
+    res["roofline"] = board_roofline(B, N, ms * 1e3, committed_pmc("r02_pmc_board_step.json", "board_kernel<6, false>", N))
     del g
     # the same rollout fused: be_board_rollout, 100 steps per launch with the state in registers
     Kc = min(100, T)
@@ -428,6 +461,12 @@ def board_leg(args, gb, dev, rank, world, stream):
                             "reward, done, truncated to (K, N, ...) buffers; bit-identical to be_board_step)",
                     "value": Tf * N * world / el, "unit": "env-steps/s", "ms_per_step": el / Tf * 1e3,
                     "kernel_us_per_step": ev0.elapsed_time(ev1) * 1e3 / Tf}
+    # fused bytes per env-step: action 1 + reward 8 + done/truncated 2 + features 80, the state once per launch
+    Bf = 1 + 8 + 2 + 80 + (2 * 44 + 28 + 24) / Kc
+    res["fused"]["bytes_per_env_step"] = Bf
+    res["fused"]["roofline"] = board_roofline(Bf, N, res["fused"]["kernel_us_per_step"],
+                                              committed_pmc("r02_pmc_board_rollout.json", "board_kernel<6, true>",
+                                                            N * Kc))
     b.close()
     return res
 
