@@ -351,6 +351,42 @@ __device__ __forceinline__ void raster_rows(const NearList<BLOCK>& nl, const Win
   }
 }
 
+// Row-span table of the fixed-shape kernels (unit cell step, agent-relative near entries, R <=
+// HW_MAX): mt[(f + R) * (R + 2) + min(ady, R + 1)] is raster_rows' row mask for an obstacle at
+// window column f (-R .. W-1+R: the near box's range) and row distance ady (0 past R), so a near
+// entry costs one LDS read per row instead of the span arithmetic.  Same masks, bit for bit.
+template <int WT>
+__device__ void build_span_table(uint16_t* mt, int R, int tid, int nthreads) {
+  const int RA = R + 2, n = (WT + 2 * R) * RA;
+  for (int x = tid; x < n; x += nthreads) {
+    const int f = x / RA - R, ady = x - (x / RA) * RA;
+    uint16_t m = 0;
+    if (ady <= R) {
+      const int hw = isqrt_small(R * R - ady * ady);   // == Tables::hw[ady] (exact floor sqrt)
+      const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
+      m = lo <= hi ? (uint16_t)((2u << hi) - (1u << lo)) : (uint16_t)0;
+    }
+    mt[x] = m;
+  }
+}
+template <int WT, int BLOCK>
+__device__ __forceinline__ void raster_rows_mt(const NearList<BLOCK>& nl, int R, uint32_t (&rows)[Geo<WT>::K],
+                                               const uint16_t* mt) {
+  constexpr int K = Geo<WT>::K;
+  static_assert(WT <= 16, "16-bit row masks");
+#pragma unroll
+  for (int k = 0; k < K; ++k) rows[k] = 0u;
+  const int RA = R + 2;
+  for (int n = 0; n < nl.cnt; ++n) {
+    int f, e;
+    nl.get(n, f, e);
+    const uint16_t* col = mt + (f + WT / 2 + R) * RA;
+    e += WT / 2;
+#pragma unroll
+    for (int k = 0; k < K; ++k) rows[k] |= col[min(abs(e - k), R + 1)];
+  }
+}
+
 // Flatten rows into prep_state4's cell order (window row r uses distinct row max(r-1,0): quirk Q1).
 template <int WT>
 __device__ __forceinline__ void flatten(const uint32_t (&rows)[Geo<WT>::K], uint32_t (&flat)[Geo<WT>::NW]) {
@@ -1929,6 +1965,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   // accesses ds_* -- an integer round trip of the pointer would turn them into flat accesses)
   constexpr int POL_OFF = ((G + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * F + 15) & ~15;
   uint8_t* pimg = smem + POL_OFF;
+  uint16_t* mt = reinterpret_cast<uint16_t*>(smem + POL_OFF);   // !POL: the row-span table (build_span_table)
 
   // ---- state into registers (straight-line, use order)
   const uint32_t tword = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid, TW - 1));
@@ -1950,6 +1987,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   WaveStats acc{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   if (slot) acc = WaveStats{slot[0], slot[1], slot[2], slot[3], slot[4], slot[5]};
   reinterpret_cast<uint32_t*>(&t)[min(tid, TW - 1)] = tword;
+  if constexpr (!POL) build_span_table<WT>(mt, p.R, tid, BLOCK_THREADS);
   int pquad = 0;          // POL: quadrant of the current obs
   bool pnz = false;       // POL: the current obs needs the dense forward (a lit cell / not one-hot)
   if constexpr (POL) {
@@ -2212,7 +2250,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       if (p.terminal_obs && valid && done) {   // obs of the terminal state, rows of reset envs (as be_step)
         const Win g(p, ax, ay);
         uint32_t rows[KR], flat[Geo<WT>::NW];
-        raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, t.hw);
+        if constexpr (POL) raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, t.hw);
+        else raster_rows_mt<WT, BLOCK_THREADS>(nl, p.R, rows, mt);
         flatten<WT>(rows, flat);
         write_row_global<WT>(p.terminal_obs + (so_n + i) * F, flat, quadrant(ax, ay, gx, gy));
       }
@@ -2238,7 +2277,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     {
       const Win g(p, ax, ay);
       uint32_t rows[KR], flat[Geo<WT>::NW];
-      raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, t.hw);
+      if constexpr (POL) raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, t.hw);   // (LDS full: the image)
+      else raster_rows_mt<WT, BLOCK_THREADS>(nl, p.R, rows, mt);
 #pragma unroll
       for (int k = 0; k < KR; ++k) rows[k] |= xrows[k];
       flatten<WT>(rows, flat);
@@ -2394,6 +2434,8 @@ Launch pick_rollout(const be_config& c, bool fixed_ok) {
   if (fixed && c.window == 10) L.fn = rollout_kernel<10, FIX_NS, FIX_ND>;
   else if (fixed && c.window == 5) L.fn = rollout_kernel<5, FIX_NS, FIX_ND>;
   L.lds = ((FIX_NS + FIX_ND + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * (4 + c.window * c.window) + 15) & ~15;
+  const int R = c.radius_obstacle + c.radius_agent;
+  L.lds += (c.window + 2 * R) * (R + 2) * 2;   // the row-span table
   if (L.fn) snprintf(L.name, sizeof L.name, "rollout_kernel<%d, %d, %d, 0, 1, 10>", c.window, FIX_NS, FIX_ND);
   return L;
 }
