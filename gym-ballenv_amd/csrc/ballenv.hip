@@ -1965,7 +1965,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   // accesses ds_* -- an integer round trip of the pointer would turn them into flat accesses)
   constexpr int POL_OFF = ((G + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * F + 15) & ~15;
   uint8_t* pimg = smem + POL_OFF;
-  uint16_t* mt = reinterpret_cast<uint16_t*>(smem + POL_OFF);   // !POL: the row-span table (build_span_table)
+  // the row-span table (build_span_table): after the stage, or (POL) after the chunk partials
+  uint16_t* mt = reinterpret_cast<uint16_t*>(POL ? pimg + PL.lds + POL_CHUNKS * NWAVE * 16 * NO * 4 : smem + POL_OFF);
 
   // ---- state into registers (straight-line, use order)
   const uint32_t tword = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid, TW - 1));
@@ -1987,7 +1988,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   WaveStats acc{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   if (slot) acc = WaveStats{slot[0], slot[1], slot[2], slot[3], slot[4], slot[5]};
   reinterpret_cast<uint32_t*>(&t)[min(tid, TW - 1)] = tword;
-  if constexpr (!POL) build_span_table<WT>(mt, p.R, tid, BLOCK_THREADS);
+  build_span_table<WT>(mt, p.R, tid, BLOCK_THREADS);
   int pquad = 0;          // POL: quadrant of the current obs
   bool pnz = false;       // POL: the current obs needs the dense forward (a lit cell / not one-hot)
   if constexpr (POL) {
@@ -2248,10 +2249,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     const unsigned long long m = __ballot(valid && done && p.autoreset);
     if (m) {
       if (p.terminal_obs && valid && done) {   // obs of the terminal state, rows of reset envs (as be_step)
-        const Win g(p, ax, ay);
         uint32_t rows[KR], flat[Geo<WT>::NW];
-        if constexpr (POL) raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, t.hw);
-        else raster_rows_mt<WT, BLOCK_THREADS>(nl, p.R, rows, mt);
+        raster_rows_mt<WT, BLOCK_THREADS>(nl, p.R, rows, mt);
         flatten<WT>(rows, flat);
         write_row_global<WT>(p.terminal_obs + (so_n + i) * F, flat, quadrant(ax, ay, gx, gy));
       }
@@ -2275,10 +2274,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     PH(6);
     // ---- observation (prep_state4) into this wave's stage, then 64 rows out
     {
-      const Win g(p, ax, ay);
       uint32_t rows[KR], flat[Geo<WT>::NW];
-      if constexpr (POL) raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, t.hw);   // (LDS full: the image)
-      else raster_rows_mt<WT, BLOCK_THREADS>(nl, p.R, rows, mt);
+      raster_rows_mt<WT, BLOCK_THREADS>(nl, p.R, rows, mt);
 #pragma unroll
       for (int k = 0; k < KR; ++k) rows[k] |= xrows[k];
       flatten<WT>(rows, flat);
@@ -2454,6 +2451,8 @@ Launch pick_policy_rollout(const be_config& c, bool fixed_ok, int HT, int KS, in
   L.lds = (FIX_NS + FIX_ND + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * (4 + c.window * c.window);
   L.lds = ((L.lds + 15) & ~15) + PL.lds;
   L.lds = ((L.lds + 15) & ~15) + POL_CHUNKS * (BLOCK_THREADS / 64) * 16 * NO * 4;   // chunk partials
+  const int R = c.radius_obstacle + c.radius_agent;
+  L.lds += (c.window + 2 * R) * (R + 2) * 2;   // the row-span table (3.2 KB at W = 10, R = 25: fits the CU's 160 KB)
   return L;
 }
 
