@@ -282,15 +282,16 @@ def policy_roofline(args, gb, dev, rank, pol, us_per_step, chunk, img):
            "mfma_per_tile": mfma_per_tile, "int8_ops_issued_per_step": ops_step,
            "hbm_bytes_per_env_step": B, "hbm_GBs": B * N / (us_per_step * 1e-6) / 1e9,
            "hbm_frac": B * N / (us_per_step * 1e-6) / 1e9 / HBM_PEAK_GBS,
-           "limiter": "neither roofline: VALU-issue/latency-bound at one wave per SIMD (the 89-KB policy image in "
-                      "LDS leaves room for one 4-wave block per CU): env physics, select_action's softmax/draw and "
-                      "the head FMAs of the dense tiles"}
+           "limiter": "neither roofline: VALU-issue/latency-bound at one wave per SIMD (65536 envs in 256-thread "
+                      "blocks are one block per CU, and the 89-KB policy image leaves LDS for only one): env "
+                      "physics, select_action's softmax/draw and the head FMAs of the dense tiles"}
     # counters of the same kernel / envs / chunk (tools/pmc_passes.sh + tools/pmc_report.py, committed profile)
     pmc = os.path.join(ROOT, "profiles", "r02_pmc_policy_rollout.json")
     if os.path.exists(pmc):
         d = json.load(open(pmc))
         if d.get("units_per_dispatch") == N * chunk and f"rollout_kernel<{W}, 13, 5, {HT}, {KS}," in (d.get("kernel") or ""):
-            res.update({"traffic": d["hbm_bytes_per_unit"] * N, "traffic_per_env_step": d["hbm_bytes_per_unit"],
+            res.update({"traffic": d["hbm_bytes_per_dispatch"], "traffic_unit": f"HBM bytes per launch ({chunk} steps)",
+                        "traffic_per_env_step": d["hbm_bytes_per_unit"],
                         "valu_active_frac": d.get("valu_active_per_simd_frac_est"),
                         "mfma_busy_frac": d.get("mfma_busy_frac_est"),
                         "lds_bank_conflict_frac": d.get("lds_bank_conflict_frac"),
