@@ -120,6 +120,51 @@ int main(int argc, char** argv) {
     for (int p = 0; p < 3; ++p)
       if (!fx[p].empty())
         printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", fn[p], pct(fx[p], .5), pct(fx[p], .9), pct(fx[p], .99), pct(fx[p], 1));
+    if (rep == 2) {   // the tail: which waves end last, and where their time went
+      std::vector<unsigned> hw(DW);
+      be_diag_hwid(hw.data());
+      std::vector<int> idx;
+      for (int w = 0; w < DW; ++w) if (rt[w * DP + 0]) idx.push_back(w);
+      std::sort(idx.begin(), idx.end(), [&](int a, int b) { return rt[a * DP + 6] > rt[b * DP + 6]; });
+      std::vector<double> end_r, end_n;
+      std::vector<std::vector<double>> end_x(16);
+      for (int w : idx) {
+        const unsigned long long* r = &rt[w * DP];
+        const bool rs = r[12] >= r[0] && r[12] <= r[6] && r[12];
+        (rs ? end_r : end_n).push_back((r[6] - t0) * 0.01);
+        end_x[(hw[w] >> 28) & 15].push_back((r[6] - t0) * 0.01);
+      }
+      printf("  tail: end us of reset waves (%zu) p50 %.2f max %.2f | other waves (%zu) p50 %.2f p90 %.2f p99 %.2f max %.2f\n",
+             end_r.size(), end_r.empty() ? 0 : pct(end_r, .5), end_r.empty() ? 0 : pct(end_r, 1), end_n.size(), pct(end_n, .5),
+             pct(end_n, .9), pct(end_n, .99), pct(end_n, 1));
+      for (int x = 0; x < 16; ++x)
+        if (!end_x[x].empty()) printf("  tail: xcc %d end p50 %.2f p90 %.2f max %.2f us\n", x, pct(end_x[x], .5), pct(end_x[x], .9), pct(end_x[x], 1));
+      {   // -DBE_RESET_STAMPS builds: reset waves' phase A split (2 -> 7 -> 8 -> 9 -> 10 -> 12)
+        std::vector<std::vector<double>> ra(5);
+        for (int w : idx) {
+          const unsigned long long* r = &rt[w * DP];
+          const unsigned long long* c = &cy[w * DP];
+          if (!(r[12] >= r[0] && r[12] <= r[6] && r[12]) || !(c[7] > c[2] && c[8] >= c[7] && c[9] >= c[8] && c[10] >= c[9] && c[12] >= c[10])) continue;
+          ra[0].push_back((double)(c[7] - c[2])); ra[1].push_back((double)(c[8] - c[7])); ra[2].push_back((double)(c[9] - c[8]));
+          ra[3].push_back((double)(c[10] - c[9])); ra[4].push_back((double)(c[12] - c[10]));
+        }
+        const char* rn[5] = {"stores->pass setup", "philox", "goal/agent block", "broadcast", "->stamp12"};
+        if (!ra[0].empty())
+          for (int q = 0; q < 5; ++q)
+            printf("  reset A: %-20s cycles p50 %6.0f max %6.0f (%zu waves)\n", rn[q], pct(ra[q], .5), pct(ra[q], 1), ra[q].size());
+      }
+      printf("  tail: the 24 last waves (start, end us; reset; xcc/se/cu; cycles per phase 0-1 1-2 2-3 3-4 4-5 5-6)\n");
+      for (int n = 0; n < 24 && n < (int)idx.size(); ++n) {
+        const int w = idx[n];
+        const unsigned long long* r = &rt[w * DP];
+        const unsigned long long* c = &cy[w * DP];
+        const unsigned h = hw[w];
+        printf("    w%5d %.2f %.2f %s x%u/se%u/cu%2u |", w, (r[0] - t0) * 0.01, (r[6] - t0) * 0.01,
+               (r[12] >= r[0] && r[12] <= r[6] && r[12]) ? "R" : "-", (h >> 28) & 15, (h >> 13) & 3, (h >> 8) & 15);
+        for (int p = 0; p < 6; ++p) printf(" %6llu", c[p + 1] - c[p]);
+        printf("\n");
+      }
+    }
   }
   return 0;
 }
