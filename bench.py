@@ -60,6 +60,8 @@ def parse():
                    help="config 5 leg: timed steps of the on-GPU policy rollout (0 = skip)")
     p.add_argument("--torch-policy-steps", type=int, default=50,
                    help="config 5 comparison: timed steps with the PyTorch-ROCm policy (0 = skip)")
+    p.add_argument("--cold-steps", type=int, default=2000,
+                   help="steps of the cold-action-rows line (a fresh tape read from HBM; 0 = skip)")
     p.add_argument("--rollout-steps", type=int, default=1000,
                    help="fused be_rollout leg (SURVEY 8(d) fused multi-step mode): timed steps (0 = skip)")
     p.add_argument("--rollout-chunk", type=int, default=100, help="steps per be_rollout launch")
@@ -142,6 +144,38 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el, ev0.elapsed_time(ev1) / steps
+
+
+def cold_actions_leg(args, env, lib, dev, stream, world, B):
+    """The headline step on action rows that come from HBM.  The headline's K rows are replayed by
+    the untimed settle pass first, so they sit in the Infinity Cache -- as actions a policy writes
+    just before each step do.  Here: a fresh (steps, N) tape that no step has read, and a 512-MB
+    write before the timed pass evicts the caches, so every step's 64-KB row is an HBM miss."""
+    import ctypes as C
+    import torch
+    T, N, chunk = args.cold_steps, env.num_envs, 250
+    tape = env.sample_actions(T, seed=0xC01D)
+    st_ref, out_ref = C.byref(env._st), C.byref(env._out)
+    graphs = []
+    cap = torch.cuda.Stream(dev)
+    for c0 in range(0, T, chunk):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            cs = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            for t in range(c0, min(T, c0 + chunk)):
+                rc = lib.be_step(env._ctx, st_ref, C.c_void_p(tape[t].data_ptr()), None, None, out_ref, cs)
+                if rc:
+                    raise RuntimeError(f"be_step: {rc}")
+        graphs.append(g)
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    flush.fill_(1)
+    el, ms = timed_graph_steps(graphs, T, dev, stream, world)
+    del graphs, flush
+    env.status()
+    return {"what": f"the headline step, {T} steps on a fresh action tape read from HBM (caches flushed by a "
+                    "512-MB write before the timed pass); the headline's rows are Infinity-Cache resident",
+            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
+            "kernel_us_mean": ms * 1e3, "frac": B * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def policy_leg(args, gb, dev, rank, world, stream):
@@ -620,6 +654,7 @@ def main():
         if d.get("envs") == N and d.get("window") == W and f"::{kname}(" in (d.get("kernel") or ""):
             traffic, traffic_src = d.get("hbm_bytes_per_launch"), "committed profile " + os.path.relpath(pmc, ROOT)
 
+    cold_res = cold_actions_leg(args, env, lib, dev, stream, world, B) if args.cold_steps > 0 else None
     pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
     board_res = board_leg(args, gb, dev, rank, world, stream) if args.board_steps > 0 else None
     roll_res = rollout_leg(args, gb, dev, rank, world, stream) if args.rollout_steps > 0 else None
@@ -646,6 +681,7 @@ def main():
                          "kernel": kname, "traffic_source": traffic_src},
             "cpu_baseline": base,
             "episodes": ep,
+            "cold_action_rows": cold_res,
             "policy_rollout": pol_res,
             "board_profile": board_res,
             "fused_rollout": roll_res,
