@@ -72,23 +72,25 @@ int main(int argc, char** argv) {
     const char* names[6] = {"entry->barrier1 (loads)", "barrier1->physics", "physics->reset list", "list->stage written", "stage->after coop reset", "coop reset->end(copy)"};
     for (int p = 0; p < 6; ++p)
       printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", names[p], pct(ph[p], .5), pct(ph[p], .9), pct(ph[p], .99), pct(ph[p], 1));
-    std::vector<std::vector<double>> sub(4);
+    std::vector<std::vector<double>> sub(5);
     for (int w = 0; w < DW; ++w) {
-      if (!rt[w * DP + 0] || !cy[w * DP + 8]) continue;
-      // step2_kernel stamps 8 -> 7 (Philox) -> 11 (dynamic) -> 10 (static), no point 9
-      const unsigned long long c9 = cy[w * DP + 9] ? cy[w * DP + 9] : cy[w * DP + 11];
-      sub[0].push_back((double)(cy[w * DP + 8] - cy[w * DP + 1]));
-      sub[1].push_back((double)(c9 - cy[w * DP + 8]));
-      sub[2].push_back((double)(cy[w * DP + 10] - c9));
-      sub[3].push_back((double)(cy[w * DP + 2] - cy[w * DP + 10]));
+      const unsigned long long* c = &cy[w * DP];
+      // step2_kernel stamps 1 -> 7 (counter, Philox) -> 11 (dynamic moves) -> 8 (action, move,
+      // distance) -> 10 (obstacle tests) -> 2 (reward, stores)
+      if (!rt[w * DP + 0] || !(c[7] > c[1] && c[11] >= c[7] && c[8] >= c[11] && c[10] >= c[8] && c[2] >= c[10])) continue;
+      sub[0].push_back((double)(c[7] - c[1])); sub[1].push_back((double)(c[11] - c[7]));
+      sub[2].push_back((double)(c[8] - c[11])); sub[3].push_back((double)(c[10] - c[8]));
+      sub[4].push_back((double)(c[2] - c[10]));
     }
-    const char* sn[4] = {"  physics: action+move", "  physics: dynamic obs", "  physics: static obs", "  physics: reward+stores"};
-    for (int p = 0; p < 4; ++p)
-      printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", sn[p], pct(sub[p], .5), pct(sub[p], .9), pct(sub[p], .99), pct(sub[p], 1));
+    const char* sn[5] = {"  physics: counter+philox", "  physics: dynamic moves", "  physics: action+distance",
+                         "  physics: obstacle tests", "  physics: reward+stores"};
+    for (int p = 0; p < 5; ++p)
+      if (!sub[p].empty())
+        printf("  %-26s cycles p50 %8.0f p90 %8.0f p99 %8.0f max %8.0f\n", sn[p], pct(sub[p], .5), pct(sub[p], .9), pct(sub[p], .99), pct(sub[p], 1));
     // fixed-shape kernels: 8 -> 7 Philox, 7 -> 11 dynamic moves + their tests, 11 -> 9 static tests
     std::vector<std::vector<double>> fx(3);
     for (int w = 0; w < DW; ++w) {
-      if (!rt[w * DP + 0] || !cy[w * DP + 7] || !cy[w * DP + 11]) continue;
+      if (!rt[w * DP + 0] || !cy[w * DP + 7] || !cy[w * DP + 11] || cy[w * DP + 8] > cy[w * DP + 7]) continue;   // be_kernel order
       fx[0].push_back((double)(cy[w * DP + 7] - cy[w * DP + 8]));
       fx[1].push_back((double)(cy[w * DP + 11] - cy[w * DP + 7]));
       fx[2].push_back((double)((cy[w * DP + 9] ? cy[w * DP + 9] : cy[w * DP + 10]) - cy[w * DP + 11]));
