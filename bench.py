@@ -70,7 +70,39 @@ def parse():
                         "multi-rank path with several ranks sharing one GPU")
     p.add_argument("--board-steps", type=int, default=1000,
                    help="createBoard profile leg (SURVEY 8(f) rank 2): timed steps (0 = skip)")
+    p.add_argument("--config2-steps", type=int, default=1000,
+                   help="BASELINE config 2 leg (4096 envs/GPU, W=5, step API): timed steps (0 = skip)")
+    p.add_argument("--config2-envs", type=int, default=4096)
+    p.add_argument("--large-steps", type=int, default=200,
+                   help="large-batch leg (2^20 envs/GPU, W=10: past the 256-MB Infinity Cache): timed steps "
+                        "(0 = skip)")
+    p.add_argument("--large-envs", type=int, default=1 << 20)
+    p.add_argument("--from-reset-steps", type=int, default=400,
+                   help="the headline step timed straight from a fresh reset (no settle): timed steps (0 = skip)")
     return p.parse_args()
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) run outside torch.distributed.run: start
+    `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a CHILD process (never an
+    exec; nothing here has touched a GPU), relay its output (rank 0 prints the JSON line) and
+    return its exit code.  The driver's own form (torchrun ... bench.py --gpus N) sets WORLD_SIZE
+    and never comes here."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    print(f"bench: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return p.wait()
 
 
 def host_cores():
@@ -404,6 +436,98 @@ def rollout_leg(args, gb, dev, rank, world, stream):
     return res
 
 
+def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, chunk=250):
+    """be_step of N envs/GPU at window W, T steps replayed from hipGraphs of captured launches
+    (the headline's method), after `settle` untimed steps since reset (0: timed straight from
+    the reset).  Returns (result dict, kernel name); the env is closed."""
+    import ctypes as C
+    import torch
+    from gym_ballenv_amd import _abi
+    cfg = gb.EnvConfig()
+    env = gb.BatchedBallEnv(N, W, cfg, device=dev, seed=seed, env_offset=rank * N)
+    acts = env.sample_actions(T, seed=seed)
+    lib, ctx, st, out = env._lib, env._ctx, C.byref(env._st), C.byref(env._out)
+    graphs, cap = [], torch.cuda.Stream(dev)
+    env.reset()
+    for c0 in range(0, T, chunk):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            cs = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            for t in range(c0, min(T, c0 + chunk)):
+                rc = lib.be_step(ctx, st, C.c_void_p(acts[t].data_ptr()), None, None, out, cs)
+                if rc:
+                    _abi.check(rc, ctx)
+        graphs.append(g)
+    untimed = 0
+    while True:          # the first replay uploads the graphs; then settle (or reset again)
+        for g in graphs:
+            g.replay()
+        untimed += T
+        if untimed >= max(settle, 1):
+            break
+    if settle <= 0:
+        env.reset()      # timed straight from a fresh reset (in place: the graphs' buffers)
+        untimed = 0
+    torch.cuda.synchronize(dev)
+    el, ms = timed_graph_steps(graphs, T, dev, stream, world)
+    env.status()
+    kname = env.kernel_name("step")
+    del graphs
+    env.close()
+    B = gb.survey_step_bytes(cfg, W)
+    B_eng = gb.step_bytes(cfg, W)
+    us = ms * 1e3
+    res = {"value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3, "steps": T,
+           "untimed_steps_since_reset": untimed, "envs_per_gpu": N, "window": W, "kernel": kname,
+           "kernel_us_mean": us,
+           "roofline": {"bound": "hbm", "bytes_per_env_step": B, "achieved": B * N / (us * 1e-6) / 1e9,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": B * N / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                        "engine_bytes_per_env_step": B_eng,
+                        "engine_frac": B_eng * N / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "measured_frac": None}}
+    return res, kname
+
+
+def add_measured(rf, pmc, us):
+    """roofline.traffic / measured_frac from a committed PMC profile (bytes per launch)."""
+    if pmc:
+        t = pmc["hbm_bytes_per_dispatch"]
+        rf.update({"traffic": t, "measured_GBs": t / (us * 1e-6) / 1e9,
+                   "measured_frac": t / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic_source": pmc["source"]})
+    return rf
+
+
+def config2_leg(args, gb, dev, rank, world, stream):
+    """BASELINE config 2: 4096 envs/GPU at W=5, random actions, the step API (one be_step launch
+    per step, graph-replayed, 1000 timed steps after the settle), SURVEY 8(d): 315 B/env-step."""
+    N, W = args.config2_envs, 5
+    res, kname = graph_steps_leg(gb, dev, rank, world, stream, N, W, args.config2_steps, args.settle)
+    res["workload"] = (f"BASELINE config 2: BallEnv step + prep_state4, random actions, {N} envs/GPU, W=5, 13 static "
+                       "+ 5 dynamic obstacles, TimeLimit 1000, autoreset, hipGraph replay of be_step launches")
+    add_measured(res["roofline"], committed_pmc("r03_pmc_config2.json", kname, N), res["kernel_us_mean"])
+    return res
+
+
+def large_batch_leg(args, gb, dev, rank, world, stream):
+    """The headline step at 2^20 envs/GPU (W=10): ~300 MB of state and outputs, past the 256-MB
+    Infinity Cache, so the PMC bytes are DRAM traffic (SURVEY 8(d) caveat)."""
+    N, W = args.large_envs, args.window
+    res, kname = graph_steps_leg(gb, dev, rank, world, stream, N, W, args.large_steps, args.large_steps,
+                                 chunk=args.large_steps)
+    res["workload"] = (f"the headline step at {N} envs/GPU, W={W} (working set past the Infinity Cache), "
+                       "hipGraph replay of be_step launches")
+    add_measured(res["roofline"], committed_pmc("r03_pmc_large_batch.json", kname, N), res["kernel_us_mean"])
+    return res
+
+
+def from_reset_leg(args, gb, dev, rank, world, stream):
+    """The headline step timed straight from a fresh reset, no settle (round-1 bench method): the
+    first ~300 steps of a fresh batch run ~7.0 -> 6.6 us (many early collisions, more resets)."""
+    res, _ = graph_steps_leg(gb, dev, rank, world, stream, args.envs, args.window, args.from_reset_steps, 0)
+    res["workload"] = "the headline step, timed from a fresh reset (no untimed settle)"
+    return res
+
+
 def committed_pmc(fname, kernel_sub, units):
     """A committed tools/pmc_report.py profile, if it was taken on this kernel at this many units
     per dispatch (else None)."""
@@ -508,9 +632,14 @@ def board_leg(args, gb, dev, rank, world, stream):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU: "
+                         f"torchrun --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}, or bench.py --gpus N alone)")
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -655,6 +784,9 @@ def main():
             traffic, traffic_src = d.get("hbm_bytes_per_launch"), "committed profile " + os.path.relpath(pmc, ROOT)
 
     cold_res = cold_actions_leg(args, env, lib, dev, stream, world, B) if args.cold_steps > 0 else None
+    c2_res = config2_leg(args, gb, dev, rank, world, stream) if args.config2_steps > 0 else None
+    large_res = large_batch_leg(args, gb, dev, rank, world, stream) if args.large_steps > 0 else None
+    fresh_res = from_reset_leg(args, gb, dev, rank, world, stream) if args.from_reset_steps > 0 else None
     pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
     board_res = board_leg(args, gb, dev, rank, world, stream) if args.board_steps > 0 else None
     roll_res = rollout_leg(args, gb, dev, rank, world, stream) if args.rollout_steps > 0 else None
@@ -678,10 +810,17 @@ def main():
                          "bytes_per_env_step": B, "bytes_source": "SURVEY.md 8(d): 82+8*Ns+20*Nd+4+W^2",
                          "engine_bytes_per_env_step": B_eng, "engine_achieved": achieved_eng,
                          "engine_frac": achieved_eng / HBM_PEAK_GBS, "kernel_us_mean": kern_ms * 1e3,
-                         "kernel": kname, "traffic_source": traffic_src},
+                         "kernel": kname, "traffic_source": traffic_src,
+                         "measured_frac": (traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                         "measured_note": "measured_frac = PMC bytes per launch (2 x FETCH_SIZE + WRITE_SIZE) / kernel "
+                                          "time / 8 TB/s; at 65 536 envs those bytes are Infinity-Cache (MALL) "
+                                          "fabric requests, not DRAM: see large_batch for a DRAM-resident point"},
             "cpu_baseline": base,
             "episodes": ep,
             "cold_action_rows": cold_res,
+            "config2": c2_res,
+            "large_batch": large_res,
+            "from_reset": fresh_res,
             "policy_rollout": pol_res,
             "board_profile": board_res,
             "fused_rollout": roll_res,

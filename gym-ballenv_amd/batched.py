@@ -266,7 +266,7 @@ class BatchedBallEnv:
     def kernel_name(self, entry: str = "step") -> Optional[str]:
         """Name of the kernel an entry point launches for this env (rocprofv3's kernel name
         without namespace / arguments): entry in step (caller actions), step_sampled,
-        rollout (None: be_rollout loops be_step), reset, observe."""
+        rollout (None when be_rollout falls back to looping be_step), reset, observe."""
         ids = {"step": 0, "step_sampled": 1, "rollout": 2, "reset": 3, "observe": 4}
         r = self._lib.be_kernel_name(self._ctx, ids[entry])
         return r.decode() if r else None

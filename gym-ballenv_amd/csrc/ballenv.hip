@@ -2474,8 +2474,26 @@ struct be_ctx {
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
   bool step_lpe1;      // the one-lane-per-env fixed step kernel instead of step2_kernel (see below)
+  int max_lds;         // the device's LDS bytes per workgroup
+  mutable struct { KFn fn; int lds; bool ok; } lds_cache[4];   // fits_lds() answers per (kernel, dynamic LDS)
   char err[512];
 };
+
+// Does a fused kernel's LDS (static + this launch's dynamic bytes) fit one workgroup?  The fused
+// rollouts' dynamic LDS grows with R = radius_obstacle + radius_agent (near lists, row-span
+// table) and the config-5 kernel is within 72 B of the CU's 160 KB at the default R = 25, so a
+// larger R must take the per-step fallback instead of failing the launch.
+static bool fits_lds(const be_ctx* ctx, const Launch& L) {
+  if (!L.fn) return false;
+  for (auto& c : ctx->lds_cache)
+    if (c.fn == L.fn && c.lds == L.lds) return c.ok;
+  hipFuncAttributes fa;
+  bool ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(L.fn)) == hipSuccess &&
+            (int64_t)fa.sharedSizeBytes + L.lds <= (int64_t)ctx->max_lds;
+  for (auto& c : ctx->lds_cache)
+    if (!c.fn) { c.fn = L.fn; c.lds = L.lds; c.ok = ok; break; }
+  return ok;
+}
 
 static thread_local char g_err[512];
 
@@ -2608,7 +2626,7 @@ const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
   switch (entry) {
     case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, !ctx->step_lpe1); break;
     case BE_ENTRY_STEP_SAMPLED: L = pick_kernel(ctx->cfg, MODE_STEP, false); break;
-    case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok); break;
+    case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok); if (!fits_lds(ctx, L)) L.fn = nullptr; break;
     case BE_ENTRY_RESET: L = pick_kernel(ctx->cfg, MODE_RESET, false); break;
     case BE_ENTRY_OBSERVE: L = pick_kernel(ctx->cfg, MODE_OBSERVE, false); break;
     default: return nullptr;
@@ -2676,7 +2694,13 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     ctx->step_lpe1 = (int64_t)cfg->num_envs > (int64_t)96 * 4 * cus;
   }
-  if (const char* l = getenv("BALLENV_STEP_LPE")) ctx->step_lpe1 = atoi(l) == 1;
+  if (const char* l = getenv("BALLENV_STEP_LPE")) {   // A/B override: exactly "1" or "2", else ignored
+    if (!strcmp(l, "1")) ctx->step_lpe1 = true;
+    else if (!strcmp(l, "2")) ctx->step_lpe1 = false;
+  }
+  if (hipDeviceGetAttribute(&ctx->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess ||
+      ctx->max_lds <= 0)
+    ctx->max_lds = 65536;
   Tables& t = ctx->tables;
   memset(&t, 0, sizeof t);
   for (int k = 0; k < cfg->num_dynamic; ++k) t.speed[k] = cfg->obstacle_speed[k];
@@ -2820,7 +2844,7 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
     return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs a 16-byte aligned obs and num_envs * (4+W*W) % 16 == 0");
   if (steps == 0) return BE_OK;
   const Launch L = pick_rollout(ctx->cfg, !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals);
-  if (L.fn) {
+  if (fits_lds(ctx, L)) {
     KParams a = make_params(ctx, st, out);
     a.actions = actions; a.steps = steps;
     int cur = -1;
@@ -2851,7 +2875,7 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
 int be_internal_policy_rollout(be_ctx* ctx, const be_state* st, const be_pol_rollout_args* r, void* stream) {
   const Launch L = pick_policy_rollout(ctx->cfg, !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals, r->HT,
                                        r->KS, r->NO);
-  if (!L.fn) return 0;
+  if (!fits_lds(ctx, L)) return 0;   // the caller loops select_action + be_step instead
   KParams a = make_params(ctx, st, r->out);
   a.steps = r->steps;
   a.pol_bytes = r->img_bytes; a.pol_actions = r->num_actions; a.pol_img = r->img; a.pol_seed = r->seed;

@@ -156,7 +156,7 @@ const char* be_last_error(const be_ctx* ctx);
  * bad ctx / entry.  No GPU work.  Diagnostics only; the reference has no counterpart. */
 enum { BE_ENTRY_STEP_ACTIONS = 0,   /* be_step with caller action indices           */
        BE_ENTRY_STEP_SAMPLED = 1,   /* be_step with in-kernel sampled actions       */
-       BE_ENTRY_ROLLOUT = 2,        /* be_rollout (NULL name: it loops be_step)     */
+       BE_ENTRY_ROLLOUT = 2,        /* be_rollout (NULL when it falls back to looping be_step) */
        BE_ENTRY_RESET = 3, BE_ENTRY_OBSERVE = 4 };
 const char* be_kernel_name(const be_ctx* ctx, int32_t entry);
 

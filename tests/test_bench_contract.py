@@ -26,7 +26,8 @@ def test_cpu_baseline_leg_small_sample():
 @pytest.mark.gpu
 def test_bench_json_line(gpu):
     cmd = [sys.executable, "bench.py", "--steps", "20", "--warmup", "5", "--settle", "60", "--no-cpu-baseline",
-           "--policy-steps", "20", "--torch-policy-steps", "5", "--board-steps", "20", "--rollout-steps", "100"]
+           "--policy-steps", "20", "--torch-policy-steps", "5", "--board-steps", "20", "--rollout-steps", "100",
+           "--config2-steps", "50", "--large-steps", "20", "--from-reset-steps", "20"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -39,6 +40,50 @@ def test_bench_json_line(gpu):
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9 and rf["kernel"] == "step2_kernel<10, 13, 5>"
     assert rf["traffic"] is None or rf["traffic"] > 0
-    for leg in ("policy_rollout", "fused_rollout", "board_profile"):
+    for leg in ("policy_rollout", "fused_rollout", "board_profile", "config2", "large_batch", "from_reset"):
         assert d[leg]["value"] > 0, leg
+    assert d["config2"]["envs_per_gpu"] == 4096 and d["config2"]["window"] == 5
+    assert d["config2"]["roofline"]["bytes_per_env_step"] == 315
+    assert d["large_batch"]["envs_per_gpu"] == 1 << 20 and d["large_batch"]["steps"] == 20
+    assert d["from_reset"]["untimed_steps_since_reset"] == 0
     assert "cpu_baseline" not in d or d["cpu_baseline"] is None
+
+
+_ONLY_HEADLINE = ["--no-cpu-baseline", "--policy-steps", "0", "--board-steps", "0", "--rollout-steps", "0",
+                  "--cold-steps", "0", "--config2-steps", "0", "--large-steps", "0", "--from-reset-steps", "0"]
+
+
+def _bench_line(args, timeout=110):
+    r = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]      # rank 0 only
+    return json.loads(lines[0])
+
+
+def test_bench_gpus_mismatch_refused():
+    """--gpus N inside a launch of another world size fails loudly (no silent one-rank run)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *_ONLY_HEADLINE], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "--gpus 2 but WORLD_SIZE=1" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_multi_rank_gloo(gpu):
+    """`bench.py --gpus 2` starts two ranks itself (a child torch.distributed.run; gloo here, so
+    both share the one GPU) and runs bench.py's own multi-rank path end to end: barrier + max
+    over ranks of the timed region, the all_gather of the stats records, the device count.  The
+    two ranks' combined episodes equal a one-rank run over the same global env ids."""
+    common = ["--steps", "20", "--warmup", "5", "--settle", "60", *_ONLY_HEADLINE]
+    d2 = _bench_line(["--gpus", "2", "--dist-backend", "gloo", "--envs", "4096", *common])
+    assert d2["ranks"] == 2 and d2["n_gpus"] == 1
+    assert d2["config"]["envs_per_gpu"] == 4096 and d2["config"]["global_envs"] == 8192
+    assert d2["value"] > 0 and d2["roofline"]["kernel"] == "step2_kernel<10, 13, 5>"
+    d1 = _bench_line(["--gpus", "1", "--envs", "8192", *common])
+    assert d1["ranks"] == 1 and d1["config"]["global_envs"] == 8192
+    e1, e2 = d1["episodes"], d2["episodes"]
+    assert e1["episodes"] > 0 and e2["episodes"] == e1["episodes"]
+    assert e2["min_return"] == e1["min_return"] and e2["max_return"] == e1["max_return"]
+    assert e2["mean_return"] == pytest.approx(e1["mean_return"], rel=1e-12)
+    assert e2["mean_length"] == pytest.approx(e1["mean_length"], rel=1e-12)

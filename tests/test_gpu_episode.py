@@ -250,8 +250,8 @@ def test_step_kernel_dispatch_by_batch(gpu, monkeypatch):
     e.close()
 
 
-@pytest.mark.parametrize("N,tl", [(20000, 20), (65536, 1000), (1000, 7)])
-def test_step2_equals_one_lane_kernel(gpu, N, tl, monkeypatch):
+@pytest.mark.parametrize("N,tl,f32", [(20000, 20, False), (65536, 1000, False), (1000, 7, False), (4000, 20, True)])
+def test_step2_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
     """step2_kernel (two lanes per env) equals the one-lane fixed-shape kernel bit for bit --
     obs, reward, done, truncated, final return / length, terminal obs, the state and the
     stats slots -- through mass truncation (tl=20: every env of every wave resets on the same
@@ -262,7 +262,7 @@ def test_step2_equals_one_lane_kernel(gpu, N, tl, monkeypatch):
     envs = []
     for lpe in ("2", "1"):
         monkeypatch.setenv("BALLENV_STEP_LPE", lpe)
-        envs.append(make_env(cfg_py, N, W, gpu, seed=31, terminal_obs=True))
+        envs.append(make_env(cfg_py, N, W, gpu, seed=31, terminal_obs=True, obs_f32=f32))
     monkeypatch.delenv("BALLENV_STEP_LPE")
     assert envs[0].kernel_name("step") == "step2_kernel<10, 13, 5>"
     assert envs[1].kernel_name("step") == "be_kernel<10, 0, 13, 5>"
@@ -284,6 +284,9 @@ def test_step2_equals_one_lane_kernel(gpu, N, tl, monkeypatch):
                 np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=f"variant {v} t={t}")
             for key in ("truncated", "terminal_obs"):
                 np.testing.assert_array_equal(res[0][3][key].cpu().numpy(), res[v][3][key].cpu().numpy(), err_msg=key)
+            if f32:   # step2_kernel's f32 copy-out (copy_out<64>) against the one-lane kernel's and the u8 obs
+                np.testing.assert_array_equal(envs[0].obs_f32.cpu().numpy(), envs[v].obs_f32.cpu().numpy())
+                np.testing.assert_array_equal(envs[0].obs_f32.cpu().numpy(), res[0][0].cpu().numpy().astype(np.float32))
             for key in ("final_return", "final_len"):
                 np.testing.assert_array_equal(res[0][3][key].cpu().numpy()[d], res[v][3][key].cpu().numpy()[d])
             s1 = np_state(envs[v])

@@ -222,3 +222,19 @@ def test_policy_rollout_crowded_multi_round(gpu):
         e.status()
         r.close()
         e.close()
+
+
+@pytest.mark.parametrize("r_obs", [21, 58])
+def test_fused_rollouts_non_default_radius(gpu, r_obs):
+    """A larger collision radius R = radius_obstacle + radius_agent grows the fused kernels' LDS
+    (near lists, row-span table).  At R >= 26 the config-5 kernel no longer fits the CU's 160 KB,
+    so be_policy_rollout must take its two-launch fallback instead of failing the launch; the
+    random-action rollout still fits at R = 63 and stays fused.  Both equal the per-step paths."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg = EnvConfig(radius_obstacle=r_obs, time_limit=40)
+    e = make_env(cfg, 4096, 10, gpu, seed=3)
+    assert e.kernel_name("rollout") == "rollout_kernel<10, 13, 5, 0, 1, 10>"
+    e.close()
+    _run_pair(cfg, 4096, 10, 40, (15, 25), terminal=True)
+    n_done, lit = _policy_pair(cfg, 4096, 10, 30, 30, True)
+    assert lit > 0
