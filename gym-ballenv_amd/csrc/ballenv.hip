@@ -1926,6 +1926,297 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   DIAG(6);
 }
 
+// ------------------------------------------------------------------ small batches at W = 5
+// stepw_kernel<5, NS, ND, L>: the fixed-shape step of be_kernel<5, MODE_STEP, NS, ND>, bit for
+// bit, with L (4 or 8) lanes per env, for BASELINE config 2 (4 096 envs, W=5).  With one lane
+// per env 4 096 envs are 16 blocks: 64 waves on a 1 024-SIMD chip, each wave running the whole
+// per-env chain for 64 envs.  Here a block is 32 envs (one be_stats_slots slot) on 32 L lanes:
+//  * lane h of an env takes obstacles k = L j + h (at L = 8: one dynamic and two static slots,
+//    the slot past the count re-reads a real obstacle and is masked out), moves, tests and
+//    stores them, and rasterises the ones that can light a cell straight into a packed row
+//    word (W = 5: the 4 distinct rows of quirk Q1 are 20 bits, row k at bits 5k..5k+4);
+//  * the group ORs its rows and both collision flags as one word (log2 L DPP ops);
+//  * the Philox block, the agent move, the f64 distance / reward and done run on every lane of
+//    the group (the same instruction stream: no extra issue), the per-env scalar stores are
+//    spread over the group's lanes;
+//  * lane h writes bytes [4h, 4h+4) (L = 8) or [8h, 8h+8) (L = 4) of its env's obs row into the
+//    wave's LDS stage, and the wave copies its 64/L rows (a contiguous 232 / 464 B) out;
+//  * autoreset is wave_resets (the owner is the group's lane 0), as in step2_kernel;
+//  * the block's 32 envs share one stats slot: every wave leaves its finished envs' return and
+//    length in LDS, and the LAST wave of the block to finish (an LDS counter; no block barrier)
+//    folds them in env order -- the same sums, in the same order, as the one-lane kernel.
+template <int L>
+__device__ __forceinline__ uint32_t lane_group_or(uint32_t x) {   // OR over the aligned group of L lanes
+  static_assert(L == 4 || L == 8, "L must be 4 or 8");
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);     // quad_perm 1,0,3,2
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);     // quad_perm 2,3,0,1
+  if constexpr (L == 8) x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  return x;
+}
+
+template <int WT, int NSC, int NDC, int L>
+__global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
+  constexpr int CT = 32 * L, EPW = 64 / L, NWAVE = CT / 64;
+  constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;   // obstacle slots per lane
+  constexpr int KR = Geo<WT>::K, F = Geo<WT>::F;
+  constexpr int BPL = (F + L - 1) / L;                             // obs bytes per lane
+  constexpr int WB = EPW * F, SW = (WB + 15) & ~15;                // a wave's obs bytes, its stage stride
+  static_assert(WT * KR <= 20, "packed rows: 20 bits + the two collision flags");
+  static_assert(NDC <= 5, "one Philox block of 24-bit fields");
+  static_assert(16 * KR >= (64 / (NSC + NDC)) * (KR + 4), "wave reset scratch");
+  static_assert(WB % 8 == 0, "a wave's rows are whole 8-byte words");
+  __shared__ Tables t;
+  __shared__ uint32_t s_rows[NWAVE][16 * KR];      // wave_resets scratch (row masks + stash)
+  __shared__ __align__(16) uint8_t s_stage[NWAVE][SW];
+  __shared__ double s_fret[32], s_slot[6];
+  __shared__ int32_t s_flen[32];
+  __shared__ uint32_t s_fmask, s_waves;
+  constexpr int TW = (int)(sizeof(Tables) / 4);
+
+  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
+  const int el = tid / L, blk0 = (int)blockIdx.x * 32, i = blk0 + el, e0 = blk0 + w * EPW;
+  const bool valid = i < N;
+  const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
+  uint8_t* stage = &s_stage[w][0];
+
+  // ---- every load, straight-line, in use order (as step2_kernel)
+  constexpr int TL = (TW + CT - 1) / CT;
+  uint32_t tword[TL];
+#pragma unroll
+  for (int j = 0; j < TL; ++j)
+    tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid + j * CT, TW - 1));
+  const uint32_t episode = ld_s(p.episode, ic);
+  const int len0 = ld_s(p.ep_len, ic);
+  const int32_t agent0 = ld_s(p.agent, ic), goal0 = ld_s(p.goal, ic);
+  int32_t dp[SD], so[SS];
+  int dgi[SD];
+#pragma unroll
+  for (int j = 0; j < SD; ++j) {
+    const uint32_t e = (uint32_t)min(L * j + h, NDC - 1) * (uint32_t)N + ic;
+    dp[j] = ld_s(p.dyn_obs, e);
+    dgi[j] = ld_s(p.dyn_goal, e);
+  }
+#pragma unroll
+  for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
+  const double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic);
+  double ret = ld_s(p.ep_return, ic);
+  const int a = ld_s(p.actions, ic);
+  double* const slot = p.stats ? p.stats + (size_t)blockIdx.x * 8 : nullptr;
+  double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sp2 = sp0;
+  if (slot && tid == 0) {   // the block's stats slot, read now (used by whichever wave folds last)
+    sp0 = reinterpret_cast<const double2*>(slot)[0];
+    sp1 = reinterpret_cast<const double2*>(slot)[1];
+    sp2 = reinterpret_cast<const double2*>(slot)[2];
+  }
+#pragma unroll
+  for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tid + j * CT, TW - 1)] = tword[j];
+  if (tid == 0) { s_fmask = 0u; s_waves = 0u; }
+  __syncthreads();   // the only block barrier: tables staged, fold counters cleared
+
+  // ---- this lane's dynamic obstacles (ballenv_env.py:323-353): draws and moves need no action
+  int counter = (int)((double)len0 * p.inv_g1);   // counter == ep_len mod (G+1)
+  counter = len0 - counter * (p.goal_change + 1);
+  if (counter < 0) counter += p.goal_change + 1;
+  if (counter > p.goal_change) counter -= p.goal_change + 1;
+  const bool change = counter >= p.goal_change;
+  const u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+  uint32_t st_flags = 0u;
+  int ngs[SD];
+  int32_t dnew[SD];
+#pragma unroll
+  for (int j = 0; j < SD; ++j) {
+    const int k = L * j + h;
+    int ox = px(dp[j]), oy = py(dp[j]);
+    uint32_t fl = 0u;
+    ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[min(k, NDC - 1)], change, pick_field(b0, min(k, 4)), fl);
+    st_flags |= k < NDC ? fl : 0u;
+    dnew[j] = pk(ox, oy);
+  }
+  // ---- action -> agent move + clamp (ballenv_env.py:247-259); unit moves and speeds
+  st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
+  const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
+  int ax = min(max(px(agent0) + (int)((p.amx >> sh) & 3u) - 1, 0), p.screen_w);
+  int ay = min(max(py(agent0) + (int)((p.amy >> sh) & 3u) - 1, 0), p.screen_h);
+  int gx = px(goal0), gy = py(goal0);
+  const int R = p.R;
+  const uint32_t R2 = (uint32_t)(R * R);
+  const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
+  const double dist = calc_dist(gx, gy, ax, ay);
+  const double rbase = (0.0 - p.time_penalty) + (old_dist - dist) / total;
+
+  // ---- collision test, and the row masks of the obstacles that can light a cell
+  //      (prep_state4 with quirk Q1, ball_cnn_ac3.py:384-412: row k is y offset k - W/2)
+  uint32_t word = 0u;   // rows (20 bits) | static hit << 20 | dynamic hit << 21
+  auto obstacle = [&](int32_t opk, bool real, uint32_t hit_bit) {
+    const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
+    word |= (real & ((uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2)) ? hit_bit : 0u;
+    const int f = d.x + WT / 2, e = d.y + WT / 2;   // window column / distinct-row coordinates
+    if (real & ((uint32_t)(f + R) <= (uint32_t)(WT - 1 + 2 * R)) & ((uint32_t)(e + R) <= (uint32_t)(KR - 1 + 2 * R))) {
+#pragma unroll
+      for (int k = 0; k < KR; ++k) {
+        const int ady = abs(e - k);
+        const int hw = t.hw[min(ady, HW_MAX)];
+        const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
+        word |= (ady <= R && lo <= hi) ? ((2u << hi) - (1u << lo)) << (WT * k) : 0u;
+      }
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < SD; ++j) obstacle(dnew[j], L * j + h < NDC, 1u << 21);
+#pragma unroll
+  for (int j = 0; j < SS; ++j) obstacle(so[j], L * j + h < NSC, 1u << 20);
+  word = lane_group_or<L>(word);
+  const bool hs = (word >> 20) & 1u, hd = (word >> 21) & 1u;
+  uint32_t rows = word & 0xFFFFFu;
+
+  // ---- reward, done (ballenv_env.py:268-286, 200-229), on every lane of the group
+  double reward = rbase;
+  if (hs) reward -= p.static_penalty;          // statics come first in obstacle_list (Q3)
+  else if (hd) reward -= p.dynamic_penalty;
+  ret += reward;
+  const int len = len0 + 1;
+  const bool env_done = (dist < p.threshold_goal) || hs || hd;
+  const bool trunc = p.time_limit > 0 && len >= p.time_limit;
+  const bool done = env_done || trunc;
+  const bool do_reset = valid && done && p.autoreset;
+  if (valid) {   // the per-env scalars over the group's lanes: one store instruction per class
+    if (h < 3) st_wt((h == 0 ? p.reward : h == 1 ? p.ep_return : p.prev_dist) + i, h == 0 ? reward : h == 1 ? ret : dist);
+    if (h < 2) st_wt((h ? p.ep_len : p.agent) + i, h ? len : pk(ax, ay));
+    uint8_t* pb = h == 0 ? p.done : h == 1 ? p.truncated : nullptr;
+    if (pb) st_wt(pb + i, (uint8_t)(h ? (trunc && !env_done) : done));
+    if (done) {
+      if (h == 2 && p.final_return) st_wt(p.final_return + i, ret);
+      if (h == 3 && p.final_len) st_wt(p.final_len + i, len);
+    }
+#pragma unroll
+    for (int j = 0; j < SD; ++j) {
+      const int k = L * j + h;
+      if (k < NDC) {
+        st_wt(&ld_s_ptr(p.dyn_obs, (uint32_t)k * (uint32_t)N + (uint32_t)i), dnew[j]);
+        if (change) st_wt(&ld_s_ptr(p.dyn_goal, (uint32_t)k * (uint32_t)N + (uint32_t)i), (uint8_t)ngs[j]);
+      }
+    }
+  }
+  if (__ballot(st_flags != 0u)) {   // rare: OR the wave's flags, one atomic
+    uint32_t f = st_flags;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
+    if (lane == 0) atomicOr(p.status, (int)f);
+  }
+  const unsigned long long m = __ballot(do_reset && h == 0);
+
+  // ---- episode boundary: terminal obs, then the wave's resets
+  if (do_reset && p.terminal_obs && h == 0) {
+    const uint32_t fl[Geo<WT>::NW] = {(rows & ((1u << WT) - 1u)) | (rows << WT), 0u};
+    write_row_global<WT>(p.terminal_obs + (int64_t)i * F, fl, quadrant(ax, ay, gx, gy));
+  }
+  if (m) {
+    uint32_t xrows[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) xrows[k] = 0u;
+    int kept = 1;   // wave_resets zeroes it for the lanes of a reset env
+    auto osink = [&](int, int k, int il, int32_t o) {
+      if (k < NSC) {
+        st_wt(p.static_obs + (size_t)k * N + il, o);
+      } else {
+        st_wt(p.dyn_obs + (size_t)(k - NSC) * N + il, o);
+        st_wt(p.dyn_goal + (size_t)(k - NSC) * N + il, (uint8_t)(k - NSC));
+      }
+    };
+    auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
+      if (h) return;   // every lane of the group takes the new agent / goal / rows; lane 0 stores
+      st_wt(p.agent + i, ag);
+      st_wt(p.goal + i, go);
+      double prev;
+      const double td = reset_dists(ag, go, a0, prev);
+      st_wt(p.prev_dist + i, prev);
+      st_wt(p.total_dist + i, td);
+      st_wt(p.ep_return + i, 0.0);
+      st_wt(p.ep_len + i, 0);
+      st_wt(p.episode + i, episode + 1u);
+    };
+    if (!(m & (m - 1)))
+      wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
+                                                                        kept, xrows, &s_rows[w][0], osink, esink);
+    else
+      wave_resets<WT, NSC, NDC, 64, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
+                                                                         kept, xrows, &s_rows[w][0], osink, esink);
+    if (!kept) {
+      rows = 0u;
+#pragma unroll
+      for (int k = 0; k < KR; ++k) rows |= xrows[k] << (WT * k);
+    }
+  }
+
+  // ---- observation (prep_state4): lane h writes bytes [BPL h, BPL (h+1)) of its env's row
+  {
+    const int quad = quadrant(ax, ay, gx, gy);
+    const uint32_t flat = (rows & ((1u << WT) - 1u)) | (rows << WT);   // row r uses distinct row max(r-1, 0)
+    uint8_t* dst = stage + (el - w * EPW) * F;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+      const int b = BPL * h + j;
+      if (BPL * L == F || b < F) dst[b] = (uint8_t)(b < 4 ? (b == quad) : (flat >> (b - 4)) & 1u);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    const int e0u = __builtin_amdgcn_readfirstlane(e0);
+    if (e0u + EPW <= N && p.obs && !p.obs_f32) {   // the common case: the wave's rows, one store per lane
+      typedef int v2i_ __attribute__((ext_vector_type(2)));
+      typedef int v4i_ __attribute__((ext_vector_type(4)));
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.obs + (size_t)e0u * F, (short)0, WB, 0x00020000);
+      if constexpr (WB % 16 == 0) {
+        const v4i_ x = reinterpret_cast<const v4i_*>(stage)[min(lane, WB / 16 - 1)];
+        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, lane * 16, 0, BE_OBS_AUX);
+      } else {
+        const v2i_ x = reinterpret_cast<const v2i_*>(stage)[min(lane, WB / 8 - 1)];
+        __builtin_amdgcn_raw_buffer_store_b64(x, rsrc, lane * 8, 0, BE_OBS_AUX);
+      }
+    } else {   // a partial last wave, or f32 obs: byte by byte
+      const int nb = max(0, min(EPW, N - e0u)) * F;
+      for (int b = lane; b < nb; b += 64) {
+        if (p.obs) p.obs[(size_t)e0u * F + b] = stage[b];
+        if (p.obs_f32) p.obs_f32[(size_t)e0u * F + b] = (float)stage[b];
+      }
+    }
+  }
+
+  // ---- the block's stats slot: the last wave to get here folds the 32 envs in env order
+  if (slot) {
+    const bool fin = done && valid && h == 0;
+    if (fin) { s_fret[el] = ret; s_flen[el] = len; }
+    const unsigned long long fm = __ballot(fin);
+    uint32_t wm = 0u;   // this wave's finished envs as bits of the block's 32
+#pragma unroll
+    for (int g = 0; g < EPW; ++g) wm |= (uint32_t)((fm >> (g * L)) & 1ull) << (w * EPW + g);
+    uint32_t last = 0u;
+    if (lane == 0) {
+      if (tid == 0) {
+        s_slot[0] = sp0.x; s_slot[1] = sp0.y; s_slot[2] = sp1.x; s_slot[3] = sp1.y; s_slot[4] = sp2.x; s_slot[5] = sp2.y;
+      }
+      if (wm) __hip_atomic_fetch_or(&s_fmask, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      last = __hip_atomic_fetch_add(&s_waves, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == NWAVE - 1 ? 1u : 0u;
+    }
+    last = (uint32_t)__builtin_amdgcn_readlane((int)last, 0);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // every lane reads after the counter
+      const uint32_t bm = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fmask);
+      if (bm) {
+        const bool d = lane < 32 && ((bm >> (lane & 31)) & 1u);
+        const WaveStats ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
+        if (lane == 0) {
+          reinterpret_cast<double2*>(slot)[0] = make_double2(s_slot[0] + ws.n, s_slot[1] + ws.s1);
+          reinterpret_cast<double2*>(slot)[1] = make_double2(s_slot[2] + ws.s2, s_slot[3] + ws.sl);
+          reinterpret_cast<double2*>(slot)[2] = make_double2(fmin(s_slot[4], ws.mn), fmax(s_slot[5], ws.mx));
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ fused multi-step rollout
 // rollout_kernel<W, NS, ND>: p.steps consecutive be_step calls of the fixed-shape kernel in one
 // launch, for a caller-given (steps, N) action tape.  Each env's state stays in registers for
@@ -2388,7 +2679,7 @@ struct Launch { KFn fn; int epb; int lds; char name[48]; int threads = BLOCK_THR
 #endif
 constexpr int FIX_NS = BE_FIX_NS, FIX_ND = BE_FIX_ND;
 
-Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe2_ok = false) {
+Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe2_ok = false, int lpe5 = 0) {
   int W = c.window;
   const int F = 4 + W * W, nobs = c.num_static + c.num_dynamic;
   Launch L{nullptr, 0, 0, {0}};
@@ -2403,6 +2694,15 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe
     constexpr int SLOTS = (FIX_NS + 1) / 2 + (FIX_ND + 1) / 2 + 1;
     L.lds = SLOTS * S2_CT * 4 + L.epb * F;
     snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d>", FIX_NS, FIX_ND);
+    return L;
+  }
+  if (fixed && W == 5 && (lpe5 == 4 || lpe5 == 8)) {
+    // L lanes per env (stepw_kernel): 32 envs per block
+    L.fn = lpe5 == 8 ? stepw_kernel<5, FIX_NS, FIX_ND, 8> : stepw_kernel<5, FIX_NS, FIX_ND, 4>;
+    L.epb = 32;
+    L.threads = 32 * lpe5;
+    L.lds = 0;
+    snprintf(L.name, sizeof L.name, "stepw_kernel<5, %d, %d, %d>", FIX_NS, FIX_ND, lpe5);
     return L;
   }
   if (fixed && W == 10) { L.fn = be_kernel<10, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
@@ -2474,6 +2774,7 @@ struct be_ctx {
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
   bool step_lpe1;      // the one-lane-per-env fixed step kernel instead of step2_kernel (see below)
+  int step5_lpe;       // W = 5: lanes per env of the fixed step kernel (1: be_kernel; 4 / 8: stepw_kernel)
   int max_lds;         // the device's LDS bytes per workgroup
   mutable struct { KFn fn; int lds; bool ok; } lds_cache[4];   // fits_lds() answers per (kernel, dynamic LDS)
   char err[512];
@@ -2624,7 +2925,7 @@ const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
   const bool fixed_ok = !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals;
   Launch L{nullptr, 0, 0, {0}};
   switch (entry) {
-    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, !ctx->step_lpe1); break;
+    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, !ctx->step_lpe1, ctx->step5_lpe); break;
     case BE_ENTRY_STEP_SAMPLED: L = pick_kernel(ctx->cfg, MODE_STEP, false); break;
     case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok); if (!fits_lds(ctx, L)) L.fn = nullptr; break;
     case BE_ENTRY_RESET: L = pick_kernel(ctx->cfg, MODE_RESET, false); break;
@@ -2684,15 +2985,23 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   b.inv_g1 = 1.0 / ((double)cfg->goal_change_step + 1.0);
   if (const char* d = getenv("BALLENV_DEBUG_SKIP")) b.dbg = (int32_t)strtoul(d, nullptr, 0);
   if (const char* g = getenv("BALLENV_GENERIC_KERNELS")) ctx->generic_only = atoi(g) != 0;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
   {  // Two lanes per env (step2_kernel) shorten each wave's dependent chain where one lane per env
      // leaves at most ~1.5 waves per SIMD; past that the one-lane kernel has the waves to hide its
      // latency and the pair's duplicated per-env work costs more than it saves (measured on MI355X,
      // 256 CUs: step2 6.42 / 7.51 us at 65 536 / 98 304 envs against 6.97 / 7.92; one lane 8.13 /
      // 14.5 / 48.9 us at 131 072 / 262 144 / 2^20 against 8.54 / 16.2 / 52.6).
      // BALLENV_STEP_LPE=1 / 2 forces one or two lanes (A/B).
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
     ctx->step_lpe1 = (int64_t)cfg->num_envs > (int64_t)96 * 4 * cus;
+  }
+  // W = 5 (BASELINE config 2): stepw_kernel's 8 lanes per env while one lane per env would leave
+  // most of the chip idle (<= 64 envs per CU), the one-lane kernel above that.
+  ctx->step5_lpe = (int64_t)cfg->num_envs <= (int64_t)64 * cus ? 8 : 1;
+  if (const char* l = getenv("BALLENV_STEP5_LPE")) {   // A/B override: "1", "4" or "8", else ignored
+    if (!strcmp(l, "1")) ctx->step5_lpe = 1;
+    else if (!strcmp(l, "4")) ctx->step5_lpe = 4;
+    else if (!strcmp(l, "8")) ctx->step5_lpe = 8;
   }
   if (const char* l = getenv("BALLENV_STEP_LPE")) {   // A/B override: exactly "1" or "2", else ignored
     if (!strcmp(l, "1")) ctx->step_lpe1 = true;
@@ -2784,7 +3093,7 @@ static int launch(be_ctx* ctx, int mode, KParams& a, void* stream, int32_t steps
   int cur = -1;
   HIP_TRY(ctx, hipGetDevice(&cur));
   if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, !ctx->step_lpe1);
+  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, !ctx->step_lpe1, ctx->step5_lpe);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)L.threads);
   for (int32_t s = 0; s < steps; ++s) {

@@ -3,7 +3,7 @@ oracle through goal changes and the TimeLimit.
 
 The bench workload (EnvConfig() defaults, caller actions) runs the fixed-shape step kernel
 (step2_kernel<10, 13, 5> at W=10 up to 98 304 envs, be_kernel<10, 0, 13, 5> past that,
-be_kernel<5, 0, 13, 5> at W=5), the fused be_rollout kernel
+stepw_kernel<5, 13, 5, 8> at W=5 up to 64 x CUs envs), the fused be_rollout kernel
 and the fused be_policy_rollout kernel.
 Each has its own goal re-pick (newGoalList for pairwise-distinct goals, ballenv_env.py:339-353)
 and its own `ep_len mod (goal_change+1)` counter arithmetic, and all of them fold the gym
@@ -28,9 +28,14 @@ SLICE = 2048
 
 def fixed_step_kernel(W, N=0):
     """The step kernel pick_kernel selects at the defaults with caller actions: step2_kernel at
-    W=10 up to 96 x 4 x CUs envs, the one-lane fixed-shape kernel otherwise."""
-    cut = 96 * 4 * torch.cuda.get_device_properties(0).multi_processor_count
-    return "step2_kernel<10, 13, 5>" if W == 10 and N <= cut else f"be_kernel<{W}, 0, 13, 5>"
+    W=10 up to 96 x 4 x CUs envs, stepw_kernel (8 lanes per env) at W=5 up to 64 x CUs envs, the
+    one-lane fixed-shape kernel otherwise."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if W == 10 and N <= 96 * 4 * cus:
+        return "step2_kernel<10, 13, 5>"
+    if W == 5 and N <= 64 * cus:
+        return "stepw_kernel<5, 13, 5, 8>"
+    return f"be_kernel<{W}, 0, 13, 5>"
 
 
 def _random_lens(N, rng, limit=1000):
@@ -320,6 +325,56 @@ def test_step_n_equals_step_calls(gpu):
     for k in KEYS:
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
     np.testing.assert_array_equal(envs[0].stats_buf.cpu().numpy(), envs[1].stats_buf.cpu().numpy())
+    for e in envs:
+        e.status()
+        e.close()
+
+
+@pytest.mark.parametrize("N,tl,f32", [(4096, 1000, False), (4096, 20, False), (1000, 7, True), (20000, 20, False)])
+def test_stepw_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
+    """stepw_kernel (W=5, 8 and 4 lanes per env, 32-env blocks with a last-wave stats fold) equals
+    the one-lane fixed-shape kernel bit for bit -- obs (u8 and f32), reward, done, truncated,
+    final return / length, terminal obs, the state and the stats slots -- through mass truncation
+    (tl=20 / 7: every env of every wave resets on the same steps) and at the defaults from random
+    episode phases; N=1000 / 20000 leave partial blocks and a partial last wave."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig(time_limit=tl)
+    W = 5
+    envs = []
+    for lpe in ("1", "8", "4"):
+        monkeypatch.setenv("BALLENV_STEP5_LPE", lpe)
+        envs.append(make_env(cfg_py, N, W, gpu, seed=77, terminal_obs=True, obs_f32=f32))
+    monkeypatch.delenv("BALLENV_STEP5_LPE")
+    assert [e.kernel_name("step") for e in envs] == ["be_kernel<5, 0, 13, 5>", "stepw_kernel<5, 13, 5, 8>",
+                                                     "stepw_kernel<5, 13, 5, 4>"]
+    lens = torch.from_numpy(_random_lens(N, np.random.default_rng(N + tl), tl)).to(gpu)
+    for e in envs:
+        e.reset()
+        e.ep_len.copy_(lens)
+    acts = envs[0].sample_actions(45, seed=19)
+    n_done = 0
+    for t in range(45):
+        for e in envs:
+            e.terminal_obs.zero_()
+        res = [e.step(acts[t]) for e in envs]
+        d = res[0][2].cpu().numpy()
+        n_done += int(d.sum())
+        s0 = np_state(envs[0])
+        for v in (1, 2):
+            for a, b in zip(res[0][:3], res[v][:3]):
+                np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=f"variant {v} t={t}")
+            for key in ("truncated", "terminal_obs"):
+                np.testing.assert_array_equal(res[0][3][key].cpu().numpy(), res[v][3][key].cpu().numpy(), err_msg=key)
+            for key in ("final_return", "final_len"):
+                np.testing.assert_array_equal(res[0][3][key].cpu().numpy()[d], res[v][3][key].cpu().numpy()[d])
+            if f32:
+                np.testing.assert_array_equal(envs[0].obs_f32.cpu().numpy(), envs[v].obs_f32.cpu().numpy())
+            s1 = np_state(envs[v])
+            for k in KEYS:
+                np.testing.assert_array_equal(s0[k], s1[k], err_msg=f"variant {v} t={t} {k}")
+    for v in (1, 2):
+        np.testing.assert_array_equal(envs[0].stats_buf.cpu().numpy(), envs[v].stats_buf.cpu().numpy())
+    assert n_done > 0
     for e in envs:
         e.status()
         e.close()
