@@ -316,6 +316,22 @@ class BatchedBallEnv:
                 src = src.view(torch.int32)
             dst.copy_(src.to(device=self.device, dtype=dst.dtype))
 
+    def save_state(self, device=None) -> torch.Tensor:
+        """be_save_state: every env's state packed into one u8 blob (include/ballenv.h layout:
+        64-byte header, then the be_state arrays), on this env's device or ``device`` ("cpu":
+        pinned host memory).  Asynchronous on the current stream."""
+        n = int(self._lib.be_state_blob_bytes(C.byref(self._abi_cfg)))
+        dev = self.device if device is None else torch.device(device)
+        blob = torch.empty(n, dtype=torch.uint8, device=dev, pin_memory=dev.type == "cpu")
+        _abi.check(self._lib.be_save_state(self._ctx, C.byref(self._st), blob.data_ptr(), self._stream()), self._ctx)
+        return blob
+
+    def load_state(self, blob: torch.Tensor) -> None:
+        """be_load_state: restore every env's state from a save_state() blob (header checked)."""
+        if blob.dtype != torch.uint8 or not blob.is_contiguous():
+            raise ValueError("blob must be a contiguous uint8 tensor from save_state()")
+        _abi.check(self._lib.be_load_state(self._ctx, C.byref(self._st), blob.data_ptr(), self._stream()), self._ctx)
+
     def close(self) -> None:
         if self._ctx is not None:
             torch.cuda.synchronize(self.device)

@@ -2776,6 +2776,7 @@ struct be_ctx {
   bool step_lpe1;      // the one-lane-per-env fixed step kernel instead of step2_kernel (see below)
   int step5_lpe;       // W = 5: lanes per env of the fixed step kernel (1: be_kernel; 4 / 8: stepw_kernel)
   int max_lds;         // the device's LDS bytes per workgroup
+  int64_t blob_hdr[8]; // be_save_state's header (host memory that outlives the async copy)
   mutable struct { KFn fn; int lds; bool ok; } lds_cache[4];   // fits_lds() answers per (kernel, dynamic LDS)
   char err[512];
 };
@@ -3224,6 +3225,68 @@ int be_sample_actions(be_ctx* ctx, uint8_t* actions_out, int32_t steps, uint64_t
   hipLaunchKernelGGL(sample_actions_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, actions_out,
                      ctx->cfg.num_envs, steps, ctx->cfg.env_offset, ctx->cfg.num_actions, (unsigned long long)seed);
   HIP_TRY(ctx, hipGetLastError());
+  return BE_OK;
+}
+
+// ---- env-state checkpoint: header + the be_state arrays at 16-byte aligned offsets
+struct BlobLayout { int64_t off[10], bytes[10], total; };
+static BlobLayout blob_layout(const be_config* c) {
+  BlobLayout b;
+  const int64_t N = c->num_envs, ns = c->num_static, nd = c->num_dynamic;
+  const int64_t sz[10] = {4 * N, 4 * N, 8 * N, 8 * N, 8 * N, 4 * N, 4 * N, 4 * ns * N, 4 * nd * N, nd * N};
+  int64_t o = 64;
+  for (int k = 0; k < 10; ++k) { b.off[k] = o; b.bytes[k] = sz[k]; o += (sz[k] + 15) & ~15ll; }
+  b.total = o;
+  return b;
+}
+static void blob_header(const be_config* c, int64_t total, int64_t (&hdr)[8]) {
+  memset(hdr, 0, sizeof hdr);
+  memcpy(&hdr[0], "BALLENV1", 8);
+  hdr[1] = BE_ABI_VERSION; hdr[2] = c->num_envs; hdr[3] = c->num_static; hdr[4] = c->num_dynamic; hdr[5] = total;
+}
+static void state_ptrs(const be_state* st, void* (&p)[10]) {
+  p[0] = st->agent; p[1] = st->goal; p[2] = st->prev_dist; p[3] = st->total_dist; p[4] = st->ep_return;
+  p[5] = st->ep_len; p[6] = st->episode; p[7] = st->static_obs; p[8] = st->dyn_obs; p[9] = st->dyn_goal;
+}
+
+int64_t be_state_blob_bytes(const be_config* cfg) {
+  if (!cfg || cfg->num_envs < 1) return 0;
+  return blob_layout(cfg).total;
+}
+
+int be_save_state(be_ctx* ctx, const be_state* st, void* blob, void* stream) {
+  if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
+  if (int rc = check_state(ctx, st)) return rc;
+  if (!blob) return fail(ctx, BE_E_INVALID, "%s", "blob is NULL");
+  const BlobLayout L = blob_layout(&ctx->cfg);
+  blob_header(&ctx->cfg, L.total, ctx->blob_hdr);   // lives in the context: safe for an async copy
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(ctx, hipMemcpyAsync(blob, ctx->blob_hdr, sizeof ctx->blob_hdr, hipMemcpyDefault, s));
+  void* src[10];
+  state_ptrs(st, src);
+  for (int k = 0; k < 10; ++k)
+    if (L.bytes[k] > 0)
+      HIP_TRY(ctx, hipMemcpyAsync(static_cast<char*>(blob) + L.off[k], src[k], (size_t)L.bytes[k], hipMemcpyDefault, s));
+  return BE_OK;
+}
+
+int be_load_state(be_ctx* ctx, const be_state* st, const void* blob, void* stream) {
+  if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
+  if (int rc = check_state(ctx, st)) return rc;
+  if (!blob) return fail(ctx, BE_E_INVALID, "%s", "blob is NULL");
+  const BlobLayout L = blob_layout(&ctx->cfg);
+  hipStream_t s = (hipStream_t)stream;
+  int64_t got[8], want[8];
+  HIP_TRY(ctx, hipMemcpyAsync(got, blob, sizeof got, hipMemcpyDefault, s));
+  HIP_TRY(ctx, hipStreamSynchronize(s));
+  blob_header(&ctx->cfg, L.total, want);
+  if (memcmp(got, want, sizeof got) != 0)
+    return fail(ctx, BE_E_INVALID, "%s", "state blob header does not match this context (magic, ABI, N, Ns, Nd)");
+  void* dst[10];
+  state_ptrs(st, dst);
+  for (int k = 0; k < 10; ++k)
+    if (L.bytes[k] > 0)
+      HIP_TRY(ctx, hipMemcpyAsync(dst[k], static_cast<const char*>(blob) + L.off[k], (size_t)L.bytes[k], hipMemcpyDefault, s));
   return BE_OK;
 }
 

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BE_ABI_VERSION 5
+#define BE_ABI_VERSION 6
 
 #define BE_MAX_STATIC   64
 #define BE_MAX_DYNAMIC  32
@@ -213,6 +213,20 @@ int be_sample_actions(be_ctx* ctx, uint8_t* actions_out, int32_t steps, uint64_t
 
 /* Synchronise the stream and read (then clear) the device status word. */
 int be_status(be_ctx* ctx, int32_t* status_out, void* stream);
+
+/* ---- env-state checkpoint (SURVEY 8(b) be_save_state / be_load_state; the reference keeps no
+ * env checkpoint, only torch.save of the policy, examples/ball_cnn_ac3.py:637-639) ----
+ * The be_state arrays of every env packed into ONE contiguous blob of be_state_blob_bytes(cfg)
+ * bytes, in device or host memory: a 64-byte header (magic "BALLENV1", ABI version, N, Ns, Nd,
+ * blob bytes) then agent, goal, prev_dist, total_dist, ep_return, ep_len, episode, static_obs,
+ * dyn_obs, dyn_goal in be_state order, each array at a 16-byte aligned offset.
+ * be_save_state: asynchronous copies on the stream.  be_load_state: synchronises the stream to
+ * check the header (BE_E_INVALID when it does not match this context's N / Ns / Nd), then copies
+ * asynchronously.  A saved blob restores the envs bit for bit, Philox positions included
+ * (episode / ep_len key every draw).                                                        */
+int64_t be_state_blob_bytes(const be_config* cfg);
+int be_save_state(be_ctx* ctx, const be_state* st, void* blob, void* stream);
+int be_load_state(be_ctx* ctx, const be_state* st, const void* blob, void* stream);
 
 /* ---- on-GPU select_action for batched rollouts (BASELINE config 5) ----
  * Replaces, for every env at once, the caller's per-step

@@ -380,3 +380,41 @@ def test_compat_single_env(gpu):
         if d:
             break
     assert d  # TimeLimit(1000) or a collision
+
+
+@pytest.mark.gpu
+def test_save_load_state_blob_round_trip(gpu):
+    """be_save_state / be_load_state (C ABI): a blob saved mid-episode, on the device
+    and in host memory, restores every env bit for bit -- the next steps reproduce the same obs,
+    rewards, dones and state (Philox positions included); a blob of another shape is refused."""
+    from gym_ballenv_amd import BallEnvError
+    from gym_ballenv_amd.config import EnvConfig
+    N, W = 3000, 10
+    env = make_env(EnvConfig(time_limit=25), N, W, gpu, seed=21)
+    env.reset()
+    acts = env.sample_actions(60, seed=5)
+    for t in range(20):
+        env.step(acts[t])
+    dev_blob, host_blob = env.save_state(), env.save_state("cpu")
+    torch.cuda.synchronize()
+    assert dev_blob.numel() == host_blob.numel() and bytes(host_blob[:8].numpy()) == b"BALLENV1"
+    ref = []
+    for t in range(20, 60):
+        obs, r, d, _ = env.step(acts[t])
+        ref.append((obs.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy()))
+    end = np_state(env)
+    for blob in (dev_blob, host_blob):
+        env.load_state(blob)
+        for t in range(20, 60):
+            obs, r, d, _ = env.step(acts[t])
+            for x, y in zip((obs, r, d), ref[t - 20]):
+                np.testing.assert_array_equal(x.cpu().numpy(), y, err_msg=f"t={t}")
+        got = np_state(env)
+        for k in KEYS:
+            np.testing.assert_array_equal(got[k], end[k], err_msg=k)
+    other = make_env(EnvConfig(time_limit=25), N + 32, W, gpu, seed=21)
+    with pytest.raises(BallEnvError, match="header"):
+        other.load_state(dev_blob)
+    env.status()
+    env.close()
+    other.close()
