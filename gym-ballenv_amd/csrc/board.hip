@@ -40,6 +40,7 @@
 #include <new>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "ballenv.h"
@@ -104,9 +105,33 @@ struct Draws {
   }
 };
 
-// featureExtractor(state, obstacle_list, (0, 0), agent_rad) -> 20 f32 (featureExtractor.py:247-265)
-template <int MAXS>
-__device__ void features(const BParams& p, int64_t i, double ax, double ay, double gx, double gy, const int32_t (&so)[MAXS]) {
+// Lane-pair helpers (L = 2 lanes per env: lanes 2e and 2e+1 hold env e)
+template <int L>
+__device__ __forceinline__ double pair_other_f64(double v) {   // the other lane's value (L = 2)
+  static_assert(L == 2, "pairs only");
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0xB1, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int L>
+__device__ __forceinline__ double pair_lead_f64(double v) {    // the pair's lane-0 value
+  static_assert(L == 2, "pairs only");
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0xA0, 0xF, 0xF, false);   // quad_perm 0,0,2,2
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0xA0, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// featureExtractor(state, obstacle_list, (0, 0), agent_rad) -> 20 f32 (featureExtractor.py:247-265).
+// L lanes per env: lane h takes obstacles k = L j + h; dk[j] = |obstacle k - agent| (the
+// collision test's distances: the same value, sqrt(fl(dx*dx) + fl(dy*dy)) is symmetric in sign).
+// The pair's counts are exact small integers; the social-force sum adds the per-obstacle terms in
+// the reference's obstacle order on both lanes.  Lane h writes the row's float4 words h, h+L, ...
+template <int MAXS, int L>
+__device__ void features(const BParams& p, int64_t row, double ax, double ay, double gx, double gy,
+                         const double (&dk)[(MAXS + L - 1) / L], int h) {
+  constexpr int SPL = (MAXS + L - 1) / L;
   float f[20];
 #pragma unroll
   for (int k = 0; k < 20; ++k) f[k] = 0.f;
@@ -123,28 +148,45 @@ __device__ void features(const BParams& p, int64_t i, double ax, double ay, doub
   else if (ang > PI / 4 && ang < PI * 3 / 4) { if (vx > 0) f[2] = 1.f; else f[4] = 1.f; }
   else f[3] = 1.f;
   // density (:91-112), speed/orientation (:115-130), social forces (:170-193)
-  // branch-free over the MAXS slots (slots past ns are masked out), so the obstacles' f64
-  // chains (sqrt, exp) interleave; the sums keep the reference's obstacle order
-  double sf = 0.0;
+  // branch-free over this lane's slots (slots past ns are masked out), so the obstacles' f64
+  // chains (exp) interleave
+  double tk[SPL];
+  float c5 = 0.f, c6 = 0.f, c7 = 0.f, c11 = 0.f;
 #pragma unroll
-  for (int k = 0; k < MAXS; ++k) {
-    const bool real = k < p.ns;
-    const int32_t o = so[k];
-    const double ox = (double)sx(o), oy = (double)sy(o);
-    const double N = dist2(ox, oy, ax, ay) - p.r_agent - p.r_feature_obs;   // calcDistance
-    f[7] += (real && N < 1000.0) ? 1.f : 0.f;
-    f[6] += (real && N < 230.0) ? 1.f : 0.f;
-    f[5] += (real && N < 101.0) ? 1.f : 0.f;
-    f[8 + 3 * 1 + 0] += real ? 1.f : 0.f;              // orientation bin 1, speed bin 0
+  for (int j = 0; j < SPL; ++j) {
+    const bool real = L * j + h < p.ns;
+    const double N = dk[j] - p.r_agent - p.r_feature_obs;   // calcDistance
+    c7 += (real && N < 1000.0) ? 1.f : 0.f;
+    c6 += (real && N < 230.0) ? 1.f : 0.f;
+    c5 += (real && N < 101.0) ? 1.f : 0.f;
+    c11 += real ? 1.f : 0.f;                               // orientation bin 1, speed bin 0
     // a*exp(-N/b)*N*thrPart, a = 1, b = 10; -N*0.1 is within an ulp of -N/10 (exp's own
     // accuracy class; only sf's f32 value and its > 1 cut, a measure-zero boundary, see it)
     const double fsoc = exp(N * -0.1) * N * 1.5;
-    sf += (real && fsoc > 1.0) ? fsoc : 0.0;           // -> phi_SF[orientation bin 1]
+    tk[j] = (real && fsoc > 1.0) ? fsoc : 0.0;             // -> phi_SF[orientation bin 1]
   }
-  f[17 + 1] = (float)sf;
-  float4* row = reinterpret_cast<float4*>(p.features + (int64_t)i * 20);   // 80-B rows: 5 x 16 B
+  double sf = 0.0;
+  if constexpr (L == 1) {
 #pragma unroll
-  for (int k = 0; k < 5; ++k) row[k] = make_float4(f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
+    for (int j = 0; j < SPL; ++j) sf += tk[j];
+  } else {
+    c5 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c5), 0xB1, 0xF, 0xF, false));
+    c6 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c6), 0xB1, 0xF, 0xF, false));
+    c7 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c7), 0xB1, 0xF, 0xF, false));
+    c11 += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, c11), 0xB1, 0xF, 0xF, false));
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {   // obstacle order: k = 2j (lane 0's), then 2j + 1 (lane 1's)
+      const double o = pair_other_f64<L>(tk[j]);
+      sf += h ? o : tk[j];
+      sf += h ? tk[j] : o;
+    }
+  }
+  f[5] = c5; f[6] = c6; f[7] = c7; f[8 + 3 * 1 + 0] = c11;
+  f[17 + 1] = (float)sf;
+  float4* out = reinterpret_cast<float4*>(p.features + row * 20);   // 80-B rows: 5 x 16 B
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    if (k % L == h) out[k] = make_float4(f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
 }
 
 // createBoard.reset for env i (ballenv_pygame.py:460-513)
@@ -342,13 +384,19 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
   }
 }
 
-// MAXS: compile-time bound on the static-obstacle count (8 / 16 / 32), so the obstacle
-// loops unroll with a runtime guard and the positions stay in registers (no scratch).
-template <int MAXS, bool ROLL = false>
+// MAXS: compile-time bound on the static-obstacle count (4 .. 32), so the obstacle loops unroll
+// with a runtime guard and the positions stay in registers (no scratch).  L lanes per env (1 or
+// 2): every lane holds the env's whole state; lane h runs the collision test and the feature
+// terms of obstacles k = L j + h (the pair combines them, above), the per-env chains (distance,
+// reward, the goal features) run on both lanes, and the pair splits the stores.  Two lanes give
+// two waves per SIMD at 65 536 envs where one lane per env leaves one.
+template <int MAXS, bool ROLL, int L>
 __global__ __launch_bounds__(256) void board_kernel(BParams p) {
+  constexpr int SPL = (MAXS + L - 1) / L;
   // every lane of a wave stays to the end (the Philox resets are wave-cooperative); lanes past
   // N work on a clamped index and store nothing
-  const int i0 = blockIdx.x * 256 + threadIdx.x;
+  const int h = (int)(threadIdx.x & (L - 1));
+  const int i0 = blockIdx.x * (256 / L) + (int)threadIdx.x / L;
   const bool valid = i0 < p.n;
   const int i = valid ? i0 : p.n - 1;
   int32_t so[MAXS];
@@ -357,20 +405,31 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   const double2 ag = reinterpret_cast<const double2*>(p.agent)[i];
   const double2 gl = reinterpret_cast<const double2*>(p.goal)[i];
   double ax = ag.x, ay = ag.y, gx = gl.x, gy = gl.y;
+  double dk[SPL];   // this lane's obstacle distances |obstacle - agent|
+  auto obstacle_dists = [&]() {
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+      const int32_t o = so[min(L * j + h, MAXS - 1)];
+      dk[j] = dist2(ax, ay, (double)sx(o), (double)sy(o));
+    }
+  };
   if (p.mode == 2) {
-    if (valid) features(p, i, ax, ay, gx, gy, so);
+    obstacle_dists();
+    if (valid) features<MAXS, L>(p, i, ax, ay, gx, gy, dk, h);
     return;
   }
   uint32_t episode = p.episode[i];
   double total = p.total[i], ret = p.ep_return[i], dist = p.dist[i];
   int32_t len = p.ep_len[i];
   bool was_reset = false;   // goal / total / episode / statics changed: store them at the end
+  bool fresh = true;        // dist may differ from |agent - goal| (a reset's state[2], or loaded state)
   // mode 3 (be_board_rollout): p.steps steps with the state in registers, per-step outputs in
   // (steps, N, ...) rows; modes 0 / 1 are one pass of the same body
   const int steps = ROLL ? p.steps : 1;   // ROLL: the mode-3 instantiation
   for (int s = 0; s < steps; ++s) {
     const int64_t row = (int64_t)s * p.n + i;   // this step's output row (i for modes 0 / 1)
     bool do_reset = valid && p.mode == 1 && (!p.mask || p.mask[i]);
+    bool moved = false;
     if (p.mode != 1) {
       double dx = 0.0, dy = 0.0;
       if (p.actions) {
@@ -380,7 +439,8 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       } else {
         dx = p.deltas[2 * row]; dy = p.deltas[2 * row + 1];
       }
-      const double old = dist2(ax, ay, gx, gy);                    // self.old_dist (:652)
+      // self.old_dist (:652) = |agent - goal|, which the previous step of this launch left in dist
+      const double old = fresh ? dist2(ax, ay, gx, gy) : dist;
       double nx = ax + dx, ny = ay + dy;
       if (nx < 0) nx = 0;
       if (nx > p.W) nx = p.W;
@@ -388,29 +448,33 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       if (ny > p.H) ny = p.H;
       ax = nx; ay = ny;
       dist = dist2(ax, ay, gx, gy);                                // state[2] (:668)
+      fresh = false;
+      moved = true;
       // calc_reward (:680-706)
+      obstacle_dists();
       double r;
       bool done = false;
 #pragma unroll
-      for (int k = 0; k < MAXS; ++k)   // any hit (the reference stops at the first; the result is the same)
-        done |= (k < p.ns) & !(dist2(ax, ay, (double)sx(so[k]), (double)sy(so[k])) > p.r_collide);
+      for (int j = 0; j < SPL; ++j)   // any hit (the reference stops at the first; the result is the same)
+        done |= (L * j + h < p.ns) & !(dk[j] > p.r_collide);
+      if constexpr (L == 2) done = (__builtin_amdgcn_update_dpp(0, (int)done, 0xB1, 0xF, 0xF, false) | (int)done) != 0;
       if (done) { r = -1.0; ret += -1.0; }
       else if (dist < p.goal_thr) { done = true; r = 1.0; ret += 1.0; }
       else { r = (old - dist) / total; ret += r; }
       ++len;
       const bool trunc = !done && p.time_limit > 0 && len >= p.time_limit;
       done = done || trunc;
-      if (valid) {
-        p.reward[row] = r;
-        p.done[row] = done ? 1 : 0;
-        if (p.truncated) p.truncated[row] = trunc ? 1 : 0;
+      if (valid) {   // the pair splits the per-step stores
+        if (h == 0) p.reward[row] = r;
+        if (h == L - 1) p.done[row] = done ? 1 : 0;
+        if (h == L - 1 && p.truncated) p.truncated[row] = trunc ? 1 : 0;
       }
       do_reset = valid && done && p.autoreset;
     }
-    if (p.tape) {   // parity mode: the reference's draw order, on the env's own lane
+    if (p.tape) {   // parity mode: the reference's draw order, on the env's own lane(s)
       if (do_reset) reset_env(p, i, episode + 1u, ax, ay, gx, gy, dist, total, so);
     } else {
-      const unsigned long long m = __ballot(do_reset);
+      const unsigned long long m = __ballot(do_reset && h == 0);
       if (m) {   // several finished envs: 2 or 4 per pass (ns must fit a slot: ns <= 64 / P)
         const int nf = __popcll(m);
         const uint32_t g = (uint32_t)p.gid0 + (uint32_t)i;
@@ -421,17 +485,30 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
           else if (nf == 2 || p.ns > 8) wave_board_resets<MAXS, 2>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
           else wave_board_resets<MAXS, 4>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
         }
+        if constexpr (L == 2) {   // the owner (lane 0) took the new state: its partner copies it
+          if (__ballot(do_reset)) {
+            ax = pair_lead_f64<L>(ax); ay = pair_lead_f64<L>(ay); gx = pair_lead_f64<L>(gx); gy = pair_lead_f64<L>(gy);
+            dist = pair_lead_f64<L>(dist); total = pair_lead_f64<L>(total);
+#pragma unroll
+            for (int k = 0; k < MAXS; ++k) so[k] = __builtin_amdgcn_update_dpp(0, so[k], 0xA0, 0xF, 0xF, false);
+          }
+        }
       }
     }
     if (do_reset) {
       ++episode;
       ret = 0.0; len = 0;
       was_reset = true;
+      fresh = true;
+      obstacle_dists();
     }
-    if (valid && p.features) features(p, row, ax, ay, gx, gy, so);
+    if (valid && p.features) {
+      if (!moved) obstacle_dists();
+      features<MAXS, L>(p, row, ax, ay, gx, gy, dk, h);
+    }
   }
   if (!valid) return;
-  if (was_reset) {
+  if (was_reset && h == L - 1) {
 #pragma unroll
     for (int k = 0; k < MAXS; ++k)
       if (k < p.ns) p.statics[(int64_t)k * p.n + i] = so[k];
@@ -439,10 +516,14 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     p.total[i] = total;
     p.episode[i] = episode;
   }
-  reinterpret_cast<double2*>(p.agent)[i] = make_double2(ax, ay);
-  p.dist[i] = dist;
-  p.ep_return[i] = ret;
-  p.ep_len[i] = len;
+  if (h == 0) {
+    reinterpret_cast<double2*>(p.agent)[i] = make_double2(ax, ay);
+    p.dist[i] = dist;
+  }
+  if (h == L - 1) {
+    p.ep_return[i] = ret;
+    p.ep_len[i] = len;
+  }
 }
 
 }  // namespace
@@ -450,6 +531,7 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
 struct be_board {
   be_board_config cfg;
   int device;
+  bool lpe1;           // BALLENV_BOARD_LPE=1: one lane per env (A/B)
   int* status;
   BoardTables* d_tables;
   char err[512];
@@ -503,6 +585,7 @@ int be_board_create(const be_board_config* cfg, int32_t device, be_board** out) 
   if (!b) return bfail(nullptr, BE_E_NOMEM, "out of host memory");
   b->cfg = *cfg;
   b->device = device;
+  if (const char* l = getenv("BALLENV_BOARD_LPE")) b->lpe1 = !strcmp(l, "1");
   BoardTables t;
   memset(&t, 0, sizeof t);
   for (int a = 0; a < cfg->num_actions; ++a) { t.actions[a][0] = cfg->actions[a][0]; t.actions[a][1] = cfg->actions[a][1]; }
@@ -567,23 +650,19 @@ static int board_launch(be_board* b, const be_board_state* st, const be_board_ou
   p.r_collide = c.static_radius + c.agent_radius; p.r_feature_obs = c.obstacle_feature_radius;
   p.r_agent = c.agent_radius; p.goal_thr = c.goal_threshold; p.min_spawn = c.min_spawn_dist;
   p.thr_agent = c.spawn_thresh_agent; p.thr_goal = c.spawn_thresh_goal;
-  // the obstacle loops run MAXS slots branch-free: the smallest bound that covers num_static
+  // the obstacle loops run MAXS slots branch-free: the smallest bound that covers num_static;
+  // two lanes per env (BALLENV_BOARD_LPE=1 forces one, for A/B) except in tape (parity) resets
+  const int lpe = (tape || b->lpe1) ? 1 : 2;
   void (*fn)(BParams) = nullptr;
-  if (mode == 3)
-    fn = c.num_static <= 4    ? board_kernel<4, true>
-         : c.num_static <= 6  ? board_kernel<6, true>
-         : c.num_static <= 8  ? board_kernel<8, true>
-         : c.num_static <= 12 ? board_kernel<12, true>
-         : c.num_static <= 16 ? board_kernel<16, true>
-                              : board_kernel<32, true>;
-  else
-    fn = c.num_static <= 4    ? board_kernel<4>
-         : c.num_static <= 6  ? board_kernel<6>
-         : c.num_static <= 8  ? board_kernel<8>
-         : c.num_static <= 12 ? board_kernel<12>
-         : c.num_static <= 16 ? board_kernel<16>
-                              : board_kernel<32>;
-  hipLaunchKernelGGL(fn, dim3((unsigned)((c.num_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p);
+#define BE_BOARD_PICK(R, LL)                                                                   \
+  fn = c.num_static <= 4 ? board_kernel<4, R, LL> : c.num_static <= 6 ? board_kernel<6, R, LL>  \
+     : c.num_static <= 8 ? board_kernel<8, R, LL> : c.num_static <= 12 ? board_kernel<12, R, LL> \
+     : c.num_static <= 16 ? board_kernel<16, R, LL> : board_kernel<32, R, LL>
+  if (mode == 3) { if (lpe == 2) BE_BOARD_PICK(true, 2); else BE_BOARD_PICK(true, 1); }
+  else { if (lpe == 2) BE_BOARD_PICK(false, 2); else BE_BOARD_PICK(false, 1); }
+#undef BE_BOARD_PICK
+  const int epb = 256 / lpe;
+  hipLaunchKernelGGL(fn, dim3((unsigned)((c.num_envs + epb - 1) / epb)), dim3(256), 0, (hipStream_t)stream, p);
   e = hipGetLastError();
   if (e != hipSuccess) return bhip(b, e);
   return BE_OK;

@@ -227,3 +227,36 @@ def test_gpu_board_philox_resets_vs_oracle(gpu, ns):
     assert n_done > N // 50, n_done
     b.status()
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ns", [6, 13])
+def test_gpu_board_two_lanes_equal_one_lane(gpu, ns, monkeypatch):
+    """The two-lanes-per-env board kernels (the default) equal the one-lane ones bit for bit:
+    features (exactly, including the social-force sum, added in obstacle order), rewards, dones
+    and state through Philox autoresets, for be_board_step, be_board_rollout and observe; a
+    partial last block (N = 5000)."""
+    N, K = 5000, 40
+    boards = []
+    for lpe in ("1", "2"):
+        monkeypatch.setenv("BALLENV_BOARD_LPE", lpe)
+        boards.append(make_board(gpu, N, ns, seed=8, autoreset=True, time_limit=25))
+    monkeypatch.delenv("BALLENV_BOARD_LPE")
+    for b in boards:
+        b.reset()
+    g = torch.Generator(device="cpu").manual_seed(ns)
+    mv = torch.randint(0, 4, (2 * K, N), generator=g, dtype=torch.uint8).to(gpu)
+    for t in range(K):
+        res = [b.step(mv[t]) for b in boards]
+        for x, y in zip(res[0][:3], res[1][:3]):
+            assert torch.equal(x, y), t
+    res = [b.rollout(mv[K:]) for b in boards]
+    for x, y in zip(res[0][:3], res[1][:3]):
+        assert torch.equal(x, y)
+    assert bool(res[0][2].any())
+    for k in boards[0].STATE_KEYS:
+        assert torch.equal(getattr(boards[0], k), getattr(boards[1], k)), k
+    assert torch.equal(boards[0].observe(), boards[1].observe())
+    for b in boards:
+        b.status()
+        b.close()
