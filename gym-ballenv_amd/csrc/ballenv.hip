@@ -41,6 +41,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <algorithm>
 #include <new>
 #include <stdint.h>
 #include <stdio.h>
@@ -101,6 +102,8 @@ struct KParams {
   // fixed-shape kernels only (pick_kernel checks the preconditions):
   uint32_t amx, amy;           // action a's (dx+1, dy+1) at bits 2a..2a+1 (every move in {-1,0,1})
   int32_t num_goals;           // goals pairwise distinct: newGoalList(g)[pick] = pick + (pick >= g)
+  int32_t prev_read;           // 1: read prev_dist; 0: no reset can re-sample the agent (Q9), so
+                               // prev_dist == calc_dist(goal, agent) and the step recomputes it
   int32_t steps;               // rollout_kernel: steps per launch (actions / outputs are (steps, N, ...))
   // fused policy rollouts (rollout_kernel with HT > 0, be_policy_rollout)
   int32_t pol_bytes, pol_actions;
@@ -1074,7 +1077,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     for (int j = 0; j < NDC; ++j) { dp[j] = ld_s(p.dyn_obs + (size_t)j * N, ic); dgi[j] = ld_s(p.dyn_goal + (size_t)j * N, ic); }
 #pragma unroll
     for (int j = 0; j < NSC; ++j) so[j] = ld_s(p.static_obs + (size_t)j * N, ic);
-    old_dist = ld_s(p.prev_dist, ic);
+    old_dist = p.prev_read ? ld_s(p.prev_dist, ic) : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
     total = ld_s(p.total_dist, ic);
     ret = ld_s(p.ep_return, ic);
   } else {
@@ -1703,7 +1706,9 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   }
 #pragma unroll
   for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
-  const double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic);
+  // state[2] of the last step (prev_read = 0: recomputed, it is calc_dist(goal, agent) -- see KParams)
+  const double old_dist = p.prev_read ? ld_s(p.prev_dist, ic) : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
+  const double total = ld_s(p.total_dist, ic);
   double ret = ld_s(p.ep_return, ic);
   // the action last: the obstacle draws and moves below need no action, so a row that misses the
   // caches (a pre-sampled action tape) delays only the work that needs it (6.46 -> 6.37 us with
@@ -1973,6 +1978,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   __shared__ uint32_t s_fmask, s_waves;
   constexpr int TW = (int)(sizeof(Tables) / 4);
 
+  if (DBG(DBG_EXIT_ENTRY)) return;
   const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
   const int el = tid / L, blk0 = (int)blockIdx.x * 32, i = blk0 + el, e0 = blk0 + w * EPW;
   const bool valid = i < N;
@@ -1998,7 +2004,8 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   }
 #pragma unroll
   for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
-  const double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic);
+  const double old_dist = p.prev_read ? ld_s(p.prev_dist, ic) : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
+  const double total = ld_s(p.total_dist, ic);
   double ret = ld_s(p.ep_return, ic);
   const int a = ld_s(p.actions, ic);
   double* const slot = p.stats ? p.stats + (size_t)blockIdx.x * 8 : nullptr;
@@ -2012,6 +2019,11 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tid + j * CT, TW - 1)] = tword[j];
   if (tid == 0) { s_fmask = 0u; s_waves = 0u; }
   __syncthreads();   // the only block barrier: tables staged, fold counters cleared
+  if (DBG(DBG_EXIT_BARRIER)) {   // diagnostics: the loads issued, nothing else
+    if (valid && (agent0 ^ goal0 ^ so[0] ^ dp[0] ^ len0 ^ a ^ (int)old_dist ^ (int)ret) == 0x7fffffff) p.obs[i] = 1;
+    return;
+  }
+  if (DBG(DBG_WAIT_LOADS)) __builtin_amdgcn_s_waitcnt(0);
 
   // ---- this lane's dynamic obstacles (ballenv_env.py:323-353): draws and moves need no action
   int counter = (int)((double)len0 * p.inv_g1);   // counter == ep_len mod (G+1)
@@ -2019,7 +2031,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   if (counter < 0) counter += p.goal_change + 1;
   if (counter > p.goal_change) counter -= p.goal_change + 1;
   const bool change = counter >= p.goal_change;
-  const u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+  const u4 b0 = DBG(DBG_NO_PHILOX) ? u4{gid, episode, 7u, 9u} : philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
   uint32_t st_flags = 0u;
   int ngs[SD];
   int32_t dnew[SD];
@@ -2103,7 +2115,8 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
     if (lane == 0) atomicOr(p.status, (int)f);
   }
-  const unsigned long long m = __ballot(do_reset && h == 0);
+  if (DBG(DBG_EXIT_PHYSICS)) return;
+  const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && h == 0);
 
   // ---- episode boundary: terminal obs, then the wave's resets
   if (do_reset && p.terminal_obs && h == 0) {
@@ -2149,7 +2162,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   }
 
   // ---- observation (prep_state4): lane h writes bytes [BPL h, BPL (h+1)) of its env's row
-  {
+  if (!DBG(DBG_NO_OBS)) {
     const int quad = quadrant(ax, ay, gx, gy);
     const uint32_t flat = (rows & ((1u << WT) - 1u)) | (rows << WT);   // row r uses distinct row max(r-1, 0)
     uint8_t* dst = stage + (el - w * EPW) * F;
@@ -2162,7 +2175,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  {
+  if (!DBG(DBG_NO_OBS)) {
     const int e0u = __builtin_amdgcn_readfirstlane(e0);
     if (e0u + EPW <= N && p.obs && !p.obs_f32) {   // the common case: the wave's rows, one store per lane
       typedef int v2i_ __attribute__((ext_vector_type(2)));
@@ -2185,7 +2198,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   }
 
   // ---- the block's stats slot: the last wave to get here folds the 32 envs in env order
-  if (slot) {
+  if (slot && !DBG(DBG_NO_STATS)) {
     const bool fin = done && valid && h == 0;
     if (fin) { s_fret[el] = ret; s_flen[el] = len; }
     const unsigned long long fm = __ballot(fin);
@@ -2910,12 +2923,25 @@ bad:
   return fail(nullptr, BE_E_INVALID, "invalid config: %s", buf);
 }
 
+// Can a reset re-sample the agent (ballenv_env.py:121-126, quirk Q9)?  Only if some agent spawn
+// point lies closer than min_spawn_dist to some goal spawn point: with the reference's strips
+// (agent y < 10, goal y >= 480) never.  When it cannot, prev_dist (state[2]) always equals
+// calc_dist(goal, agent) -- after a step it is that distance, after a reset total_distance -- and
+// the fixed-shape step kernels recompute it instead of reading it (they still store it).
+static bool q9_possible(const be_config* c) {
+  const int64_t dx = std::max<int64_t>(0, (int64_t)(c->screen_width - c->strip_goal_x) - (c->strip_agent_x - 1));
+  const int64_t dy = std::max<int64_t>(0, (int64_t)(c->screen_height - c->strip_goal_y) - (c->strip_agent_y - 1));
+  const double D = c->min_spawn_dist;
+  return D > 0.0 && sqrt((double)(dx * dx + dy * dy)) < D;
+}
+
 int64_t be_step_bytes(const be_config* c) {
   if (!c) return 0;
   // agent R+W 8 | goal R 4 | prev_dist R+W 16 | total_dist R 8 | ep_return R+W 16 | ep_len R+W 8
   // | episode R 4 | action R 1 | reward W 8 | done W 1                                     = 74
   // | statics R 4*Ns | dyn xy R+W 8*Nd | dyn goal R 1*Nd | obs W 4+W^2
-  return 74 + 4ll * c->num_static + 9ll * c->num_dynamic + 4 + (int64_t)c->window * c->window;
+  // (the fixed-shape kernels skip the 8-B prev_dist read when no reset can re-sample the agent)
+  return (q9_possible(c) ? 74 : 66) + 4ll * c->num_static + 9ll * c->num_dynamic + 4 + (int64_t)c->window * c->window;
 }
 
 const char* be_last_error(const be_ctx* ctx) { return ctx ? ctx->err : g_err; }
@@ -2965,6 +2991,8 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   b.static_penalty = cfg->static_penalty; b.dynamic_penalty = cfg->dynamic_penalty;
   b.min_spawn_dist = cfg->min_spawn_dist; b.seed = cfg->seed;
   b.num_goals = cfg->num_goals;
+  b.prev_read = q9_possible(cfg) ? 1 : 0;
+  if (const char* r = getenv("BALLENV_PREV_READ")) { if (!strcmp(r, "1")) b.prev_read = 1; }   // A/B
   ctx->unit_moves = cfg->num_actions <= 16;
   for (int a = 0; a < cfg->num_actions && a < 16; ++a) {
     const int mx = cfg->actions[a][0], my = cfg->actions[a][1];

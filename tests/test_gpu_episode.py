@@ -378,3 +378,61 @@ def test_stepw_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
     for e in envs:
         e.status()
         e.close()
+
+
+@pytest.mark.parametrize("W,N", [(10, 4096), (5, 4096), (10, 131072)])
+def test_q9_resample_config_vs_oracle(gpu, W, N):
+    """A config where a reset CAN re-sample the agent (agent strip y < 490 overlaps the goal strip,
+    ballenv_env.py:121-126, quirk Q9: state[2] keeps the pre-resample distance): the fixed-shape
+    kernels then read prev_dist instead of recomputing it (prev_read, be_step_bytes 275 B), and
+    match the oracle through many resets (time limit 12) on a 2048-env slice."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig(strip_agent_y=490, time_limit=12)
+    rng = np.random.default_rng(W + N)
+    a = N - SLICE
+    env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, SLICE, seed=0x99, rng=rng)
+    assert env.kernel_name("step") == fixed_step_kernel(W, N)
+    acts = env.sample_actions(40, seed=3)
+    q9 = 0
+    for t in range(40):
+        out["terminal_obs"][:] = 0
+        env.terminal_obs.zero_()
+        oracle.step(cfg, st, out, actions=acts[t, a:].cpu().numpy())
+        q9 += int((st["ep_len"] == 0).sum() and (st["prev_dist"] != st["total_dist"]).sum())
+        obs, reward, done, info = env.step(acts[t])
+        _check_step(t, a, SLICE, out, obs, reward, done, info["truncated"], info["final_return"], info["final_len"],
+                    info["terminal_obs"])
+        _check_state(env, st, a, SLICE, f"t={t}")
+    assert q9 > 0, "no reset re-sampled the agent"
+    env.status()
+    env.close()
+
+
+def test_prev_dist_recompute_equals_read(gpu, monkeypatch):
+    """At the defaults no reset can re-sample the agent, so the fixed-shape kernels recompute
+    prev_dist = calc_dist(goal, agent) instead of reading it; forcing the read
+    (BALLENV_PREV_READ=1) gives the same trajectory bit for bit (65 536 envs, W=10 / 4 096, W=5)."""
+    from gym_ballenv_amd.config import EnvConfig
+    for N, W in ((65536, 10), (4096, 5)):
+        envs = []
+        for v in ("1", None):
+            if v:
+                monkeypatch.setenv("BALLENV_PREV_READ", v)
+            else:
+                monkeypatch.delenv("BALLENV_PREV_READ", raising=False)
+            envs.append(make_env(EnvConfig(), N, W, gpu, seed=41))
+        lens = torch.from_numpy(_random_lens(N, np.random.default_rng(5))).to(gpu)
+        for e in envs:
+            e.reset()
+            e.ep_len.copy_(lens)
+        acts = envs[0].sample_actions(60, seed=8)
+        for t in range(60):
+            r0, r1 = (e.step(acts[t]) for e in envs)
+            for x, y in zip(r0[:3], r1[:3]):
+                np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy(), err_msg=f"N={N} t={t}")
+        s0, s1 = np_state(envs[0]), np_state(envs[1])
+        for k in KEYS:
+            np.testing.assert_array_equal(s0[k], s1[k], err_msg=k)
+        for e in envs:
+            e.status()
+            e.close()
