@@ -102,8 +102,8 @@ struct KParams {
   // fixed-shape kernels only (pick_kernel checks the preconditions):
   uint32_t amx, amy;           // action a's (dx+1, dy+1) at bits 2a..2a+1 (every move in {-1,0,1})
   int32_t num_goals;           // goals pairwise distinct: newGoalList(g)[pick] = pick + (pick >= g)
-  int32_t prev_read;           // 1: read prev_dist; 0: no reset can re-sample the agent (Q9), so
-                               // prev_dist == calc_dist(goal, agent) and the step recomputes it
+  int32_t prev_read;           // 1: read prev_dist; 0 (A/B only, when no reset can re-sample the agent,
+                               // Q9): prev_dist == calc_dist(goal, agent), recomputed
   int32_t steps;               // rollout_kernel: steps per launch (actions / outputs are (steps, N, ...))
   // fused policy rollouts (rollout_kernel with HT > 0, be_policy_rollout)
   int32_t pol_bytes, pol_actions;
@@ -2206,16 +2206,19 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
 #pragma unroll
     for (int g = 0; g < EPW; ++g) wm |= (uint32_t)((fm >> (g * L)) & 1ull) << (w * EPW + g);
     uint32_t last = 0u;
+    if (tid == 0) {
+      s_slot[0] = sp0.x; s_slot[1] = sp0.y; s_slot[2] = sp1.x; s_slot[3] = sp1.y; s_slot[4] = sp2.x; s_slot[5] = sp2.y;
+    }
+    // LDS-only ordering: a workgroup-scope release on every address space would also wait for the
+    // wave's global stores (the obs copy-out) before the counter, 0.45 us at 4 096 envs
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     if (lane == 0) {
-      if (tid == 0) {
-        s_slot[0] = sp0.x; s_slot[1] = sp0.y; s_slot[2] = sp1.x; s_slot[3] = sp1.y; s_slot[4] = sp2.x; s_slot[5] = sp2.y;
-      }
       if (wm) __hip_atomic_fetch_or(&s_fmask, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      last = __hip_atomic_fetch_add(&s_waves, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == NWAVE - 1 ? 1u : 0u;
+      last = __hip_atomic_fetch_add(&s_waves, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == NWAVE - 1 ? 1u : 0u;
     }
     last = (uint32_t)__builtin_amdgcn_readlane((int)last, 0);
     if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // every lane reads after the counter
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // every lane reads after the counter
       const uint32_t bm = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fmask);
       if (bm) {
         const bool d = lane < 32 && ((bm >> (lane & 31)) & 1u);
@@ -2926,8 +2929,8 @@ bad:
 // Can a reset re-sample the agent (ballenv_env.py:121-126, quirk Q9)?  Only if some agent spawn
 // point lies closer than min_spawn_dist to some goal spawn point: with the reference's strips
 // (agent y < 10, goal y >= 480) never.  When it cannot, prev_dist (state[2]) always equals
-// calc_dist(goal, agent) -- after a step it is that distance, after a reset total_distance -- and
-// the fixed-shape step kernels recompute it instead of reading it (they still store it).
+// calc_dist(goal, agent) -- after a step it is that distance, after a reset total_distance -- so
+// the fixed-shape step kernels may recompute it instead of reading it (an A/B option, KParams).
 static bool q9_possible(const be_config* c) {
   const int64_t dx = std::max<int64_t>(0, (int64_t)(c->screen_width - c->strip_goal_x) - (c->strip_agent_x - 1));
   const int64_t dy = std::max<int64_t>(0, (int64_t)(c->screen_height - c->strip_goal_y) - (c->strip_agent_y - 1));
@@ -2940,8 +2943,7 @@ int64_t be_step_bytes(const be_config* c) {
   // agent R+W 8 | goal R 4 | prev_dist R+W 16 | total_dist R 8 | ep_return R+W 16 | ep_len R+W 8
   // | episode R 4 | action R 1 | reward W 8 | done W 1                                     = 74
   // | statics R 4*Ns | dyn xy R+W 8*Nd | dyn goal R 1*Nd | obs W 4+W^2
-  // (the fixed-shape kernels skip the 8-B prev_dist read when no reset can re-sample the agent)
-  return (q9_possible(c) ? 74 : 66) + 4ll * c->num_static + 9ll * c->num_dynamic + 4 + (int64_t)c->window * c->window;
+  return 74 + 4ll * c->num_static + 9ll * c->num_dynamic + 4 + (int64_t)c->window * c->window;
 }
 
 const char* be_last_error(const be_ctx* ctx) { return ctx ? ctx->err : g_err; }
@@ -2991,8 +2993,11 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   b.static_penalty = cfg->static_penalty; b.dynamic_penalty = cfg->dynamic_penalty;
   b.min_spawn_dist = cfg->min_spawn_dist; b.seed = cfg->seed;
   b.num_goals = cfg->num_goals;
-  b.prev_read = q9_possible(cfg) ? 1 : 0;
-  if (const char* r = getenv("BALLENV_PREV_READ")) { if (!strcmp(r, "1")) b.prev_read = 1; }   // A/B
+  // prev_dist is read: recomputing it (possible when q9_possible() is false) measured slower, the
+  // f64 sqrt lands on the reward's chain (step2 6.52 vs 6.38 us, stepw 4.36 vs 4.20 us, A/B in one
+  // process, profiles/r03_prev_dist_ab.txt); BALLENV_PREV_READ=0 selects it where it is exact (A/B)
+  b.prev_read = 1;
+  if (const char* r = getenv("BALLENV_PREV_READ")) { if (!strcmp(r, "0") && !q9_possible(cfg)) b.prev_read = 0; }
   ctx->unit_moves = cfg->num_actions <= 16;
   for (int a = 0; a < cfg->num_actions && a < 16; ++a) {
     const int mx = cfg->actions[a][0], my = cfg->actions[a][1];

@@ -531,7 +531,7 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
 struct be_board {
   be_board_config cfg;
   int device;
-  bool lpe1;           // BALLENV_BOARD_LPE=1: one lane per env (A/B)
+  bool lpe2;           // BALLENV_BOARD_LPE=2: two lanes per env (A/B)
   int* status;
   BoardTables* d_tables;
   char err[512];
@@ -585,7 +585,7 @@ int be_board_create(const be_board_config* cfg, int32_t device, be_board** out) 
   if (!b) return bfail(nullptr, BE_E_NOMEM, "out of host memory");
   b->cfg = *cfg;
   b->device = device;
-  if (const char* l = getenv("BALLENV_BOARD_LPE")) b->lpe1 = !strcmp(l, "1");
+  if (const char* l = getenv("BALLENV_BOARD_LPE")) b->lpe2 = !strcmp(l, "2");
   BoardTables t;
   memset(&t, 0, sizeof t);
   for (int a = 0; a < cfg->num_actions; ++a) { t.actions[a][0] = cfg->actions[a][0]; t.actions[a][1] = cfg->actions[a][1]; }
@@ -651,8 +651,10 @@ static int board_launch(be_board* b, const be_board_state* st, const be_board_ou
   p.r_agent = c.agent_radius; p.goal_thr = c.goal_threshold; p.min_spawn = c.min_spawn_dist;
   p.thr_agent = c.spawn_thresh_agent; p.thr_goal = c.spawn_thresh_goal;
   // the obstacle loops run MAXS slots branch-free: the smallest bound that covers num_static;
-  // two lanes per env (BALLENV_BOARD_LPE=1 forces one, for A/B) except in tape (parity) resets
-  const int lpe = (tape || b->lpe1) ? 1 : 2;
+  // one lane per env: two (BALLENV_BOARD_LPE=2, A/B) measured slower, 9.66 vs 9.45 us per step
+  // and 4.96 vs 3.97 us fused at 65 536 envs -- the per-env f64 chains (acos, hypot, the reward
+  // divide) run on both lanes and outweigh the halved obstacle terms (profiles/r03_board_lanes_ab.txt)
+  const int lpe = (tape || !b->lpe2) ? 1 : 2;
   void (*fn)(BParams) = nullptr;
 #define BE_BOARD_PICK(R, LL)                                                                   \
   fn = c.num_static <= 4 ? board_kernel<4, R, LL> : c.num_static <= 6 ? board_kernel<6, R, LL>  \

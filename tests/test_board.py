@@ -232,7 +232,7 @@ def test_gpu_board_philox_resets_vs_oracle(gpu, ns):
 @pytest.mark.gpu
 @pytest.mark.parametrize("ns", [6, 13])
 def test_gpu_board_two_lanes_equal_one_lane(gpu, ns, monkeypatch):
-    """The two-lanes-per-env board kernels (the default) equal the one-lane ones bit for bit:
+    """The two-lanes-per-env board kernels (BALLENV_BOARD_LPE=2, an A/B option) equal the one-lane ones bit for bit:
     features (exactly, including the social-force sum, added in obstacle order), rewards, dones
     and state through Philox autoresets, for be_board_step, be_board_rollout and observe; a
     partial last block (N = 5000)."""

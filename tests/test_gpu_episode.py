@@ -384,8 +384,7 @@ def test_stepw_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
 def test_q9_resample_config_vs_oracle(gpu, W, N):
     """A config where a reset CAN re-sample the agent (agent strip y < 490 overlaps the goal strip,
     ballenv_env.py:121-126, quirk Q9: state[2] keeps the pre-resample distance): the fixed-shape
-    kernels then read prev_dist instead of recomputing it (prev_read, be_step_bytes 275 B), and
-    match the oracle through many resets (time limit 12) on a 2048-env slice."""
+    kernels match the oracle through many such resets (time limit 12) on a 2048-env slice."""
     from gym_ballenv_amd.config import EnvConfig
     cfg_py = EnvConfig(strip_agent_y=490, time_limit=12)
     rng = np.random.default_rng(W + N)
@@ -409,13 +408,13 @@ def test_q9_resample_config_vs_oracle(gpu, W, N):
 
 
 def test_prev_dist_recompute_equals_read(gpu, monkeypatch):
-    """At the defaults no reset can re-sample the agent, so the fixed-shape kernels recompute
-    prev_dist = calc_dist(goal, agent) instead of reading it; forcing the read
-    (BALLENV_PREV_READ=1) gives the same trajectory bit for bit (65 536 envs, W=10 / 4 096, W=5)."""
+    """At the defaults no reset can re-sample the agent, so prev_dist == calc_dist(goal, agent) and
+    the fixed-shape kernels may recompute it instead of reading it (BALLENV_PREV_READ=0, an A/B
+    option: slower): the same trajectory bit for bit (65 536 envs, W=10 / 4 096, W=5)."""
     from gym_ballenv_amd.config import EnvConfig
     for N, W in ((65536, 10), (4096, 5)):
         envs = []
-        for v in ("1", None):
+        for v in ("0", None):
             if v:
                 monkeypatch.setenv("BALLENV_PREV_READ", v)
             else:
