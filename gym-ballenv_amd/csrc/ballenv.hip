@@ -2115,6 +2115,29 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
     if (lane == 0) atomicOr(p.status, (int)f);
   }
+  // ---- the block's stats slot (32 envs): every wave leaves its finished envs' return / length in
+  //      LDS and bumps a counter now (right after the physics); the wave that bumps it last folds
+  //      the 32 in env order further down, before its obs copy-out, so the slot store drains with
+  //      the obs stores instead of after them
+  uint32_t last = 0u;
+  if (slot && !DBG(DBG_NO_STATS)) {
+    const bool fin = done && valid && h == 0;
+    if (fin) { s_fret[el] = ret; s_flen[el] = len; }
+    const unsigned long long fm = __ballot(fin);
+    uint32_t wm = 0u;   // this wave's finished envs as bits of the block's 32
+#pragma unroll
+    for (int g = 0; g < EPW; ++g) wm |= (uint32_t)((fm >> (g * L)) & 1ull) << (w * EPW + g);
+    if (tid == 0) {
+      s_slot[0] = sp0.x; s_slot[1] = sp0.y; s_slot[2] = sp1.x; s_slot[3] = sp1.y; s_slot[4] = sp2.x; s_slot[5] = sp2.y;
+    }
+    // LDS-only ordering (a workgroup-scope release on every address space would also wait for the
+    // wave's global stores)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0) {
+      if (wm) __hip_atomic_fetch_or(&s_fmask, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      last = __hip_atomic_fetch_add(&s_waves, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == NWAVE - 1 ? 1u : 0u;
+    }
+  }
   if (DBG(DBG_EXIT_PHYSICS)) return;
   const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && h == 0);
 
@@ -2175,6 +2198,20 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // ---- the stats fold (the block's last wave to reach the counter; its return is long back)
+  if (slot && !DBG(DBG_NO_STATS) && __builtin_amdgcn_readlane((int)last, 0)) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // every lane reads after the counter
+    const uint32_t bm = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fmask);
+    if (bm) {
+      const bool d = lane < 32 && ((bm >> (lane & 31)) & 1u);
+      const WaveStats ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
+      if (lane == 0) {
+        reinterpret_cast<double2*>(slot)[0] = make_double2(s_slot[0] + ws.n, s_slot[1] + ws.s1);
+        reinterpret_cast<double2*>(slot)[1] = make_double2(s_slot[2] + ws.s2, s_slot[3] + ws.sl);
+        reinterpret_cast<double2*>(slot)[2] = make_double2(fmin(s_slot[4], ws.mn), fmax(s_slot[5], ws.mx));
+      }
+    }
+  }
   if (!DBG(DBG_NO_OBS)) {
     const int e0u = __builtin_amdgcn_readfirstlane(e0);
     if (e0u + EPW <= N && p.obs && !p.obs_f32) {   // the common case: the wave's rows, one store per lane
@@ -2197,40 +2234,6 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     }
   }
 
-  // ---- the block's stats slot: the last wave to get here folds the 32 envs in env order
-  if (slot && !DBG(DBG_NO_STATS)) {
-    const bool fin = done && valid && h == 0;
-    if (fin) { s_fret[el] = ret; s_flen[el] = len; }
-    const unsigned long long fm = __ballot(fin);
-    uint32_t wm = 0u;   // this wave's finished envs as bits of the block's 32
-#pragma unroll
-    for (int g = 0; g < EPW; ++g) wm |= (uint32_t)((fm >> (g * L)) & 1ull) << (w * EPW + g);
-    uint32_t last = 0u;
-    if (tid == 0) {
-      s_slot[0] = sp0.x; s_slot[1] = sp0.y; s_slot[2] = sp1.x; s_slot[3] = sp1.y; s_slot[4] = sp2.x; s_slot[5] = sp2.y;
-    }
-    // LDS-only ordering: a workgroup-scope release on every address space would also wait for the
-    // wave's global stores (the obs copy-out) before the counter, 0.45 us at 4 096 envs
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) {
-      if (wm) __hip_atomic_fetch_or(&s_fmask, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      last = __hip_atomic_fetch_add(&s_waves, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == NWAVE - 1 ? 1u : 0u;
-    }
-    last = (uint32_t)__builtin_amdgcn_readlane((int)last, 0);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // every lane reads after the counter
-      const uint32_t bm = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fmask);
-      if (bm) {
-        const bool d = lane < 32 && ((bm >> (lane & 31)) & 1u);
-        const WaveStats ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
-        if (lane == 0) {
-          reinterpret_cast<double2*>(slot)[0] = make_double2(s_slot[0] + ws.n, s_slot[1] + ws.s1);
-          reinterpret_cast<double2*>(slot)[1] = make_double2(s_slot[2] + ws.s2, s_slot[3] + ws.sl);
-          reinterpret_cast<double2*>(slot)[2] = make_double2(fmin(s_slot[4], ws.mn), fmax(s_slot[5], ws.mx));
-        }
-      }
-    }
-  }
 }
 
 // ------------------------------------------------------------------ fused multi-step rollout
