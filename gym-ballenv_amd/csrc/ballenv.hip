@@ -1948,8 +1948,8 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
 //    wave's LDS stage, and the wave copies its 64/L rows (a contiguous 232 / 464 B) out;
 //  * autoreset is wave_resets (the owner is the group's lane 0), as in step2_kernel;
 //  * the block's 32 envs share one stats slot: every wave leaves its finished envs' return and
-//    length in LDS, and the LAST wave of the block to finish (an LDS counter; no block barrier)
-//    folds them in env order -- the same sums, in the same order, as the one-lane kernel.
+//    length in LDS after the physics, and after a block barrier wave 0 folds them in env order --
+//    the same sums, in the same order, as the one-lane kernel.
 template <int L>
 __device__ __forceinline__ uint32_t lane_group_or(uint32_t x) {   // OR over the aligned group of L lanes
   static_assert(L == 4 || L == 8, "L must be 4 or 8");
@@ -1973,9 +1973,9 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   __shared__ Tables t;
   __shared__ uint32_t s_rows[NWAVE][16 * KR];      // wave_resets scratch (row masks + stash)
   __shared__ __align__(16) uint8_t s_stage[NWAVE][SW];
-  __shared__ double s_fret[32], s_slot[6];
+  __shared__ double s_fret[32];
   __shared__ int32_t s_flen[32];
-  __shared__ uint32_t s_fmask, s_waves;
+  __shared__ uint8_t s_fin[32];
   constexpr int TW = (int)(sizeof(Tables) / 4);
 
   if (DBG(DBG_EXIT_ENTRY)) return;
@@ -2010,15 +2010,14 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const int a = ld_s(p.actions, ic);
   double* const slot = p.stats ? p.stats + (size_t)blockIdx.x * 8 : nullptr;
   double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sp2 = sp0;
-  if (slot && tid == 0) {   // the block's stats slot, read now (used by whichever wave folds last)
+  if (slot && tid == 0) {   // the block's stats slot, read now (wave 0 folds into it)
     sp0 = reinterpret_cast<const double2*>(slot)[0];
     sp1 = reinterpret_cast<const double2*>(slot)[1];
     sp2 = reinterpret_cast<const double2*>(slot)[2];
   }
 #pragma unroll
   for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tid + j * CT, TW - 1)] = tword[j];
-  if (tid == 0) { s_fmask = 0u; s_waves = 0u; }
-  __syncthreads();   // the only block barrier: tables staged, fold counters cleared
+  __syncthreads();   // tables staged
   if (DBG(DBG_EXIT_BARRIER)) {   // diagnostics: the loads issued, nothing else
     if (valid && (agent0 ^ goal0 ^ so[0] ^ dp[0] ^ len0 ^ a ^ (int)old_dist ^ (int)ret) == 0x7fffffff) p.obs[i] = 1;
     return;
@@ -2116,26 +2115,23 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     if (lane == 0) atomicOr(p.status, (int)f);
   }
   // ---- the block's stats slot (32 envs): every wave leaves its finished envs' return / length in
-  //      LDS and bumps a counter now (right after the physics); the wave that bumps it last folds
-  //      the 32 in env order further down, before its obs copy-out, so the slot store drains with
-  //      the obs stores instead of after them
-  uint32_t last = 0u;
+  //      LDS right after the physics, one block barrier, and wave 0 folds the 32 in env order
+  //      before its obs work (the waves reach the barrier together: the same chain)
   if (slot && !DBG(DBG_NO_STATS)) {
     const bool fin = done && valid && h == 0;
+    s_fin[el] = fin ? 1 : 0;
     if (fin) { s_fret[el] = ret; s_flen[el] = len; }
-    const unsigned long long fm = __ballot(fin);
-    uint32_t wm = 0u;   // this wave's finished envs as bits of the block's 32
-#pragma unroll
-    for (int g = 0; g < EPW; ++g) wm |= (uint32_t)((fm >> (g * L)) & 1ull) << (w * EPW + g);
-    if (tid == 0) {
-      s_slot[0] = sp0.x; s_slot[1] = sp0.y; s_slot[2] = sp1.x; s_slot[3] = sp1.y; s_slot[4] = sp2.x; s_slot[5] = sp2.y;
-    }
-    // LDS-only ordering (a workgroup-scope release on every address space would also wait for the
-    // wave's global stores)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) {
-      if (wm) __hip_atomic_fetch_or(&s_fmask, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      last = __hip_atomic_fetch_add(&s_waves, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == NWAVE - 1 ? 1u : 0u;
+    __syncthreads();
+    if (w == 0) {
+      const bool d = lane < 32 && s_fin[lane & 31];
+      if (__ballot(d)) {
+        const WaveStats ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
+        if (lane == 0) {
+          reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
+          reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
+          reinterpret_cast<double2*>(slot)[2] = make_double2(fmin(sp2.x, ws.mn), fmax(sp2.y, ws.mx));
+        }
+      }
     }
   }
   if (DBG(DBG_EXIT_PHYSICS)) return;
@@ -2198,20 +2194,6 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // ---- the stats fold (the block's last wave to reach the counter; its return is long back)
-  if (slot && !DBG(DBG_NO_STATS) && __builtin_amdgcn_readlane((int)last, 0)) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");   // every lane reads after the counter
-    const uint32_t bm = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_fmask);
-    if (bm) {
-      const bool d = lane < 32 && ((bm >> (lane & 31)) & 1u);
-      const WaveStats ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
-      if (lane == 0) {
-        reinterpret_cast<double2*>(slot)[0] = make_double2(s_slot[0] + ws.n, s_slot[1] + ws.s1);
-        reinterpret_cast<double2*>(slot)[1] = make_double2(s_slot[2] + ws.s2, s_slot[3] + ws.sl);
-        reinterpret_cast<double2*>(slot)[2] = make_double2(fmin(s_slot[4], ws.mn), fmax(s_slot[5], ws.mx));
-      }
-    }
-  }
   if (!DBG(DBG_NO_OBS)) {
     const int e0u = __builtin_amdgcn_readfirstlane(e0);
     if (e0u + EPW <= N && p.obs && !p.obs_f32) {   // the common case: the wave's rows, one store per lane
