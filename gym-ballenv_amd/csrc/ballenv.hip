@@ -2118,9 +2118,9 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   //      LDS right after the physics, one block barrier, and wave 0 folds the 32 in env order
   //      before its obs work (the waves reach the barrier together: the same chain)
   if (slot && !DBG(DBG_NO_STATS)) {
-    const bool fin = done && valid && h == 0;
+    const bool fin = done && valid;   // (the same on every lane of the group: they all write it)
     s_fin[el] = fin ? 1 : 0;
-    if (fin) { s_fret[el] = ret; s_flen[el] = len; }
+    if (fin && h == 0) { s_fret[el] = ret; s_flen[el] = len; }
     __syncthreads();
     if (w == 0) {
       const bool d = lane < 32 && s_fin[lane & 31];
