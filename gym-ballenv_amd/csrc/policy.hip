@@ -89,15 +89,14 @@ __global__ void policy_pack_kernel(PolPack a, uint8_t* img, PolLayout L) {
       img[L.frag + ((((ht * 3 + d) * L.KS + ks) * 64 + lane) * 16 + j)] = (uint8_t)(int8_t)dig[d];
   }
   // head weights, scaled by s_k: output o < A -> action_head[o], o == NO-1 -> value_head, else 0
-  // (layout [ht][g][r][o], o padded to even: head_fma's packed pairs)
-  const int g = (m >> 2) & 3, r = m & 3, nop = L.NO + (L.NO & 1);
-  for (int o = 0; o < nop; ++o) {
+  const int g = (m >> 2) & 3, r = m & 3;
+  for (int o = 0; o < L.NO; ++o) {
     double w = 0.0;
-    if (real && o < L.NO) {
+    if (real) {
       if (o < a.A) w = a.wa[(int64_t)o * a.H + m];
       else if (o == L.NO - 1) w = a.wv[m];
     }
-    head[((ht * 4 + g) * 4 + r) * nop + o] = (float)(w * s);
+    head[((ht * 4 + g) * L.NO + o) * 4 + r] = (float)(w * s);
   }
   if (m < L.NO) hb[m] = m < a.A ? a.ba[m] : (m == L.NO - 1 ? a.bv[0] : -INFINITY);
 }

@@ -18,27 +18,6 @@ constexpr int POL_THREADS = 64 * POL_ENVS / 16;  // one wave per 16-env tile
 constexpr int POL_FIN_WAVES = POL_ENVS / 64;     // waves that run the epilogue
 
 typedef int v4i __attribute__((ext_vector_type(4)));
-typedef float v2f __attribute__((ext_vector_type(2)));
-
-// The heads of one 16-row tile row for one lane (4 hidden units h[0..3] of its env, lane group
-// g): part[o] += sum_r W'[o][16ht+4g+r] h[r], each output's FMA chain in r order, two outputs per
-// packed FMA (v_pk_fma_f32: the same per-output chain as four scalar fmaf, bit for bit).
-template <int NO>
-__device__ __forceinline__ void head_fma(const float* wrow, const float (&h)[4], v2f (&part)[(NO + 1) / 2]) {
-  constexpr int NP = (NO + 1) / 2;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const v2f hr = {h[r], h[r]};
-#pragma unroll
-    for (int op = 0; op < NP; ++op)
-      part[op] = __builtin_elementwise_fma(*reinterpret_cast<const v2f*>(wrow + r * 2 * NP + 2 * op), hr, part[op]);
-  }
-}
-template <int NO>
-__device__ __forceinline__ void unpack_parts(const v2f (&p2)[(NO + 1) / 2], float (&part)[NO]) {
-#pragma unroll
-  for (int o = 0; o < NO; ++o) part[o] = (o & 1) ? p2[o >> 1].y : p2[o >> 1].x;
-}
 
 // Packed-weight image (bytes), identical in HBM and in each workgroup's LDS.
 struct PolLayout {
@@ -50,8 +29,8 @@ __host__ __device__ constexpr PolLayout pol_layout(int HT, int KS, int NO) {
   L.HT = HT; L.KS = KS; L.NO = NO;
   L.frag = 0;                                   // [HT][3 digits, high first][KS][64 lanes][16 B] int8
   L.bias = L.frag + HT * 3 * KS * 1024;         // [HT*16] i32   bq_k = rint(b1_k / s_k)
-  L.head = L.bias + HT * 16 * 4;                // [HT][4 groups][4 r][NO even] f32  W_o,k * s_k, k = 16ht+4g+r
-  L.hbias = L.head + HT * 4 * 4 * (NO + (NO & 1)) * 4;   // [NO] f32 (pad actions: -inf; value last)
+  L.head = L.bias + HT * 16 * 4;                // [HT][4 groups][NO][4] f32  W_o,k * s_k, k = 16ht+4g+r
+  L.hbias = L.head + HT * 4 * NO * 4 * 4;       // [NO] f32 (pad actions: -inf; value last)
   L.table = L.hbias + NO * 4;                   // [4][NO] f32 raw logits of the obs e_0..e_3 (empty window)
   L.total = (L.table + 4 * NO * 4 + 15) & ~15;
   L.logits = L.total;                           // LDS only: [POL_ENVS][NO] f32 for the epilogue
@@ -112,10 +91,9 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
                                            int ht1, float (&out)[PolQ<NO>::N]) {
   constexpr PolLayout L = pol_layout(HT, KS, NO);
   const int g = lane >> 4;
-  constexpr int NP = (NO + 1) / 2;
-  v2f part2[NP];
+  float part[NO];
 #pragma unroll
-  for (int o = 0; o < NP; ++o) part2[o] = v2f{0.f, 0.f};
+  for (int o = 0; o < NO; ++o) part[o] = 0.f;
   const int n = LEN > 0 ? LEN : ht1 - ht0;
 #pragma unroll
   for (int j = 0; j < (LEN > 0 ? LEN : HT); ++j) {
@@ -143,13 +121,15 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
       h[r] = (float)(q > 0 ? q : 0);
     }
     if (!(dbg & 4)) {
-      head_fma<NO>(reinterpret_cast<const float*>(lds + L.head) + (ht * 4 + g) * 4 * 2 * NP, h, part2);
+#pragma unroll
+      for (int o = 0; o < NO; ++o) {
+        const float4 w = *(const float4*)(lds + L.head + (((ht * 4 + g) * NO + o) * 4) * 4);
+        part[o] = fmaf(w.w, h[3], fmaf(w.z, h[2], fmaf(w.y, h[1], fmaf(w.x, h[0], part[o]))));
+      }
     } else {
-      part2[0].x += h[0] + h[1] + h[2] + h[3];
+      part[0] += h[0] + h[1] + h[2] + h[3];
     }
   }
-  float part[NO];
-  unpack_parts<NO>(part2, part);
   sum_outputs<NO>(part, out);
 }
 
@@ -164,10 +144,9 @@ __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[
                                             float (&out1)[PolQ<NO>::N]) {
   constexpr PolLayout L = pol_layout(HT, KS, NO);
   const int g = lane >> 4;
-  constexpr int NP = (NO + 1) / 2;
-  v2f q0[NP], q1[NP];
+  float p0[NO], p1[NO];
 #pragma unroll
-  for (int o = 0; o < NP; ++o) { q0[o] = v2f{0.f, 0.f}; q1[o] = v2f{0.f, 0.f}; }
+  for (int o = 0; o < NO; ++o) { p0[o] = 0.f; p1[o] = 0.f; }
   const int n = LEN > 0 ? LEN : ht1 - ht0;
 #pragma unroll
   for (int j = 0; j < (LEN > 0 ? LEN : HT); ++j) {
@@ -194,13 +173,13 @@ __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[
       h0[r] = (float)(q0 > 0 ? q0 : 0);
       h1[r] = (float)(q1 > 0 ? q1 : 0);
     }
-    const float* wrow = reinterpret_cast<const float*>(lds + L.head) + (ht * 4 + g) * 4 * 2 * NP;
-    head_fma<NO>(wrow, h0, q0);
-    head_fma<NO>(wrow, h1, q1);
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      const float4 w = *(const float4*)(lds + L.head + (((ht * 4 + g) * NO + o) * 4) * 4);
+      p0[o] = fmaf(w.w, h0[3], fmaf(w.z, h0[2], fmaf(w.y, h0[1], fmaf(w.x, h0[0], p0[o]))));
+      p1[o] = fmaf(w.w, h1[3], fmaf(w.z, h1[2], fmaf(w.y, h1[1], fmaf(w.x, h1[0], p1[o]))));
+    }
   }
-  float p0[NO], p1[NO];
-  unpack_parts<NO>(q0, p0);
-  unpack_parts<NO>(q1, p1);
   sum_outputs<NO>(p0, out0);
   sum_outputs<NO>(p1, out1);
 }
