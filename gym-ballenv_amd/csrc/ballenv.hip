@@ -2218,6 +2218,293 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
 
 }
 
+// rolloutw_kernel<5, NS, ND, L>: be_rollout (p.steps consecutive steps in one launch, each env's
+// state in registers) with L lanes per env and 32-env blocks, for small batches at W=5 (BASELINE
+// config 2's 4 096 envs: the one-lane rollout_kernel runs them on 16 blocks).  The per-step body
+// is stepw_kernel's (obstacle slots k = L j + h per lane, one packed row word OR-ed over the group,
+// the per-env chains on every lane of the group, wave_resets with the owner at h = 0); the state
+// stays in registers as in rollout_kernel -- each lane holds only its own obstacles, a reset's new
+// positions reach them through a per-wave LDS stash.  Outputs are per step, in (steps, N, ...)
+// rows.  Stats: the block's 32 envs share a slot; every wave records its finished envs of each
+// step in LDS and every SC steps (and at the end) wave 0 folds them step by step, each step's in
+// env order -- rollout_kernel's per-half-wave, per-step sums, bit for bit.
+template <int WT, int NSC, int NDC, int L>
+__global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
+  constexpr int CT = 32 * L, EPW = 64 / L, NWAVE = CT / 64, G = NSC + NDC;
+  constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;
+  constexpr int KR = Geo<WT>::K, F = Geo<WT>::F;
+  constexpr int BPL = (F + L - 1) / L;
+  constexpr int WB = EPW * F, SW = (WB + 15) & ~15;
+  constexpr int SC = 32;                         // steps per stats fold
+  static_assert(WT * KR <= 20, "packed rows: 20 bits + the two collision flags");
+  static_assert(NDC <= 5, "one Philox block of 24-bit fields");
+  static_assert(16 * KR >= (64 / G) * (KR + 4) && (64 / G) * G <= 64, "wave reset scratch");
+  static_assert(WB % 8 == 0, "a wave's rows are whole 8-byte words");
+  __shared__ Tables t;
+  __shared__ uint32_t s_rows[NWAVE][16 * KR];    // wave_resets scratch (row masks + stash)
+  __shared__ int32_t s_ost[NWAVE][64];           // a reset pass's new obstacle positions [slot][k]
+  __shared__ __align__(16) uint8_t s_stage[NWAVE][SW];
+  __shared__ double s_fret[SC][32];              // finished envs' return / length per step of the fold window
+  __shared__ int32_t s_flen[SC][32];
+  __shared__ uint8_t s_fdone[SC][NWAVE];         // per step and wave: its finished envs (bit g = env g of the wave)
+  constexpr int TW = (int)(sizeof(Tables) / 4);
+
+  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
+  const int el = tid / L, blk0 = (int)blockIdx.x * 32, i = blk0 + el, e0 = blk0 + w * EPW;
+  const bool valid = i < N;
+  const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
+  uint8_t* stage = &s_stage[w][0];
+
+  // ---- state into registers (straight-line, use order); each lane its own obstacle slots
+  constexpr int TL = (TW + CT - 1) / CT;
+  uint32_t tword[TL];
+#pragma unroll
+  for (int j = 0; j < TL; ++j)
+    tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid + j * CT, TW - 1));
+  uint32_t episode = ld_s(p.episode, ic);
+  int len = ld_s(p.ep_len, ic);
+  int a = ld_s(p.actions, ic);
+  const int32_t agent0 = ld_s(p.agent, ic);
+  int32_t goal = ld_s(p.goal, ic);
+  int32_t dp[SD], so[SS];
+  int dgi[SD];
+#pragma unroll
+  for (int j = 0; j < SD; ++j) {
+    const uint32_t e = (uint32_t)min(L * j + h, NDC - 1) * (uint32_t)N + ic;
+    dp[j] = ld_s(p.dyn_obs, e);
+    dgi[j] = ld_s(p.dyn_goal, e);
+  }
+#pragma unroll
+  for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
+  double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic), ret = ld_s(p.ep_return, ic);
+  double* const slot = p.stats ? p.stats + (size_t)blockIdx.x * 8 : nullptr;   // one per 32 envs
+  WaveStats acc{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
+  if (slot && tid == 0) acc = WaveStats{slot[0], slot[1], slot[2], slot[3], slot[4], slot[5]};
+#pragma unroll
+  for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tid + j * CT, TW - 1)] = tword[j];
+  __syncthreads();   // tables staged
+
+  int ax = px(agent0), ay = py(agent0);
+  uint32_t st_flags = 0u;
+  bool was_reset = false;   // statics / goal / total / episode changed: store them at the end
+  const int R = p.R;
+  const uint32_t R2 = (uint32_t)(R * R);
+  // fold the stats window's steps [0, n) in order (wave 0; after a block barrier)
+  auto fold = [&](int n) {
+    if (w != 0) return;
+#pragma unroll 1
+    for (int u = 0; u < n; ++u) {
+      uint32_t m32 = 0u;
+#pragma unroll
+      for (int ww = 0; ww < NWAVE; ++ww) m32 |= (uint32_t)s_fdone[u][ww] << (ww * EPW);
+      if (m32 == 0u) continue;   // (uniform)
+      const bool d = lane < 32 && ((m32 >> (lane & 31)) & 1u);
+      const WaveStats ws = wave_stats(d, d ? s_fret[u][lane & 31] : 0.0, d ? s_flen[u][lane & 31] : 0);
+      acc.n += ws.n; acc.s1 += ws.s1; acc.s2 += ws.s2; acc.sl += ws.sl;
+      acc.mn = fmin(acc.mn, ws.mn); acc.mx = fmax(acc.mx, ws.mx);
+    }
+  };
+
+  for (int s = 0; s < p.steps; ++s) {
+    const size_t so_n = (size_t)s * N;
+    // next step's action: in flight while this step runs
+    const int a_next = s + 1 < p.steps ? ld_s(p.actions + so_n + N, ic) : 0;
+    const int gx = px(goal), gy = py(goal);
+    // ---- this lane's dynamic obstacles (ballenv_env.py:323-353)
+    int counter = (int)((double)len * p.inv_g1);   // counter == ep_len mod (G+1)
+    counter = len - counter * (p.goal_change + 1);
+    if (counter < 0) counter += p.goal_change + 1;
+    if (counter > p.goal_change) counter -= p.goal_change + 1;
+    const bool change = counter >= p.goal_change;
+    const u4 b0 = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+#pragma unroll
+    for (int j = 0; j < SD; ++j) {
+      const int k = L * j + h;
+      int ox = px(dp[j]), oy = py(dp[j]);
+      uint32_t fl = 0u;
+      dgi[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[min(k, NDC - 1)], change, pick_field(b0, min(k, 4)), fl);
+      st_flags |= k < NDC ? fl : 0u;
+      dp[j] = pk(ox, oy);
+    }
+    // ---- action -> agent move + clamp (ballenv_env.py:247-259)
+    st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
+    const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
+    ax = min(max(ax + (int)((p.amx >> sh) & 3u) - 1, 0), p.screen_w);
+    ay = min(max(ay + (int)((p.amy >> sh) & 3u) - 1, 0), p.screen_h);
+    const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
+    const double dist = calc_dist(gx, gy, ax, ay);
+    const double rbase = (0.0 - p.time_penalty) + (old_dist - dist) / total;
+    // ---- collision test and row masks (stepw_kernel's)
+    uint32_t word = 0u;
+    auto obstacle = [&](int32_t opk, bool real, uint32_t hit_bit) {
+      const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
+      word |= (real & ((uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2)) ? hit_bit : 0u;
+      const int f = d.x + WT / 2, e = d.y + WT / 2;
+      if (real & ((uint32_t)(f + R) <= (uint32_t)(WT - 1 + 2 * R)) & ((uint32_t)(e + R) <= (uint32_t)(KR - 1 + 2 * R))) {
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+          const int ady = abs(e - k);
+          const int hw = t.hw[min(ady, HW_MAX)];
+          const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
+          word |= (ady <= R && lo <= hi) ? ((2u << hi) - (1u << lo)) << (WT * k) : 0u;
+        }
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < SD; ++j) obstacle(dp[j], L * j + h < NDC, 1u << 21);
+#pragma unroll
+    for (int j = 0; j < SS; ++j) obstacle(so[j], L * j + h < NSC, 1u << 20);
+    word = lane_group_or<L>(word);
+    const bool hs = (word >> 20) & 1u, hd = (word >> 21) & 1u;
+    uint32_t rows = word & 0xFFFFFu;
+    // ---- reward, done (ballenv_env.py:268-286, 200-229)
+    double reward = rbase;
+    if (hs) reward -= p.static_penalty;          // statics come first in obstacle_list (Q3)
+    else if (hd) reward -= p.dynamic_penalty;
+    ret += reward;
+    ++len;
+    const bool env_done = (dist < p.threshold_goal) || hs || hd;
+    const bool trunc = p.time_limit > 0 && len >= p.time_limit;
+    const bool done = env_done || trunc;
+    old_dist = dist;
+    if (valid) {   // per-step outputs over the group's lanes
+      if (h == 0) p.reward[so_n + i] = reward;
+      if (h == 1) p.done[so_n + i] = (uint8_t)done;
+      if (h == 2 && p.truncated) p.truncated[so_n + i] = (uint8_t)(trunc && !env_done);
+      if (done) {
+        if (h == 3 && p.final_return) p.final_return[so_n + i] = ret;
+        if (h == 1 && p.final_len) p.final_len[so_n + i] = len;
+      }
+    }
+    // ---- this step's finished envs for the stats fold
+    const int u = s % SC;
+    if (slot) {
+      const bool fin = done && valid;
+      if (fin && h == 0) { s_fret[u][el] = ret; s_flen[u][el] = len; }
+      const unsigned long long fm = __ballot(fin && h == 0);
+      uint32_t wm = 0u;
+#pragma unroll
+      for (int g = 0; g < EPW; ++g) wm |= (uint32_t)((fm >> (g * L)) & 1ull) << g;
+      if (lane == 0) s_fdone[u][w] = (uint8_t)wm;
+    }
+    // ---- autoreset: terminal obs, then the wave's resets (new obstacles through the LDS stash)
+    const unsigned long long m = __ballot(valid && done && p.autoreset && h == 0);
+    if (m) {
+      if (p.terminal_obs && valid && done && h == 0) {
+        const uint32_t fl[Geo<WT>::NW] = {(rows & ((1u << WT) - 1u)) | (rows << WT), 0u};
+        write_row_global<WT>(p.terminal_obs + (so_n + i) * F, fl, quadrant(ax, ay, gx, gy));
+      }
+      uint32_t xrows[KR];
+#pragma unroll
+      for (int k = 0; k < KR; ++k) xrows[k] = 0u;
+      int kept = 1;
+      int gxr = gx, gyr = gy;
+      int32_t* ost = &s_ost[w][0];
+      auto osink = [&](int sl, int k, int, int32_t o) { ost[sl * G + k] = o; };
+      auto esink = [&](int own, int32_t ag, int32_t go, int32_t a0) {   // every lane of the env's group
+        goal = go;
+        total = reset_dists(ag, go, a0, old_dist);
+        ret = 0.0; len = 0; ++episode; was_reset = true;
+#pragma unroll
+        for (int j = 0; j < SS; ++j) so[j] = ost[own * G + min(L * j + h, NSC - 1)];
+#pragma unroll
+        for (int j = 0; j < SD; ++j) { dp[j] = ost[own * G + NSC + min(L * j + h, NDC - 1)]; dgi[j] = min(L * j + h, NDC - 1); }
+      };
+      if (!(m & (m - 1)))
+        wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gxr, gyr,
+                                                                          kept, xrows, &s_rows[w][0], osink, esink);
+      else
+        wave_resets<WT, NSC, NDC, 64, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gxr, gyr,
+                                                                           kept, xrows, &s_rows[w][0], osink, esink);
+      if (!kept) {
+        rows = 0u;
+#pragma unroll
+        for (int k = 0; k < KR; ++k) rows |= xrows[k] << (WT * k);
+      }
+    }
+    // ---- observation (prep_state4) into the wave's stage, its 64/L rows out
+    if (p.obs) {
+      const int quad = quadrant(ax, ay, px(goal), py(goal));
+      const uint32_t flat = (rows & ((1u << WT) - 1u)) | (rows << WT);
+      uint8_t* dst = stage + (el - w * EPW) * F;
+#pragma unroll
+      for (int j = 0; j < BPL; ++j) {
+        const int b = BPL * h + j;
+        if (BPL * L == F || b < F) dst[b] = (uint8_t)(b < 4 ? (b == quad) : (flat >> (b - 4)) & 1u);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int e0u = __builtin_amdgcn_readfirstlane(e0);
+      uint8_t* orow = p.obs + (so_n + (size_t)e0u) * F;
+      if (e0u + EPW <= N) {
+        typedef int v2i_ __attribute__((ext_vector_type(2)));
+        typedef int v4i_ __attribute__((ext_vector_type(4)));
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(orow, (short)0, WB, 0x00020000);
+        if constexpr (WB % 16 == 0) {
+          const v4i_ x = reinterpret_cast<const v4i_*>(stage)[min(lane, WB / 16 - 1)];
+          __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, lane * 16, 0, 0);
+        } else {
+          const v2i_ x = reinterpret_cast<const v2i_*>(stage)[min(lane, WB / 8 - 1)];
+          __builtin_amdgcn_raw_buffer_store_b64(x, rsrc, lane * 8, 0, 0);
+        }
+      } else {
+        const int nb = max(0, min(EPW, N - e0u)) * F;
+        for (int b = lane; b < nb; b += 64) orow[b] = stage[b];
+      }
+      // the next step's stage writes follow this step's stage reads
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (slot && (u == SC - 1 || s + 1 == p.steps)) {   // (uniform: every wave runs every step)
+      __syncthreads();
+      fold(u + 1);
+      __syncthreads();   // the window's LDS is free again
+    }
+    a = a_next;
+  }
+
+  // ---- state back to HBM, once
+  if (valid) {
+    if (h == 0) {
+      p.agent[i] = pk(ax, ay);
+      p.prev_dist[i] = old_dist;
+      p.ep_return[i] = ret;
+      p.ep_len[i] = len;
+      if (was_reset) {
+        p.goal[i] = goal;
+        p.total_dist[i] = total;
+        p.episode[i] = episode;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < SD; ++j) {
+      const int k = L * j + h;
+      if (k < NDC) {
+        (p.dyn_obs + (size_t)k * N)[i] = dp[j];
+        (p.dyn_goal + (size_t)k * N)[i] = (uint8_t)dgi[j];
+      }
+    }
+    if (was_reset) {
+#pragma unroll
+      for (int j = 0; j < SS; ++j) {
+        const int k = L * j + h;
+        if (k < NSC) (p.static_obs + (size_t)k * N)[i] = so[j];
+      }
+    }
+  }
+  if (slot && tid == 0) {
+    slot[0] = acc.n; slot[1] = acc.s1; slot[2] = acc.s2; slot[3] = acc.sl; slot[4] = acc.mn; slot[5] = acc.mx;
+  }
+  if (__ballot(st_flags != 0u)) {
+    uint32_t f = st_flags;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
+    if (lane == 0) atomicOr(p.status, (int)f);
+  }
+}
+
 // ------------------------------------------------------------------ fused multi-step rollout
 // rollout_kernel<W, NS, ND>: p.steps consecutive be_step calls of the fixed-shape kernel in one
 // launch, for a caller-given (steps, N) action tape.  Each env's state stays in registers for
@@ -2729,10 +3016,18 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe
 }
 
 // The fused rollout kernel for the same fixed shapes (nullptr: not applicable).
-Launch pick_rollout(const be_config& c, bool fixed_ok) {
+Launch pick_rollout(const be_config& c, bool fixed_ok, int lpe5 = 0) {
   Launch L{nullptr, BLOCK_THREADS, 0, {0}};
   const bool fixed = fixed_ok && c.num_static == FIX_NS && c.num_dynamic == FIX_ND && c.speed_x == 1 &&
                      c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
+  if (fixed && c.window == 5 && (lpe5 == 4 || lpe5 == 8)) {   // small batches: L lanes per env, 32-env blocks
+    L.fn = lpe5 == 8 ? rolloutw_kernel<5, FIX_NS, FIX_ND, 8> : rolloutw_kernel<5, FIX_NS, FIX_ND, 4>;
+    L.epb = 32;
+    L.threads = 32 * lpe5;
+    L.lds = 0;
+    snprintf(L.name, sizeof L.name, "rolloutw_kernel<5, %d, %d, %d>", FIX_NS, FIX_ND, lpe5);
+    return L;
+  }
   if (fixed && c.window == 10) L.fn = rollout_kernel<10, FIX_NS, FIX_ND>;
   else if (fixed && c.window == 5) L.fn = rollout_kernel<5, FIX_NS, FIX_ND>;
   L.lds = ((FIX_NS + FIX_ND + 1) * BLOCK_THREADS * 4 + BLOCK_THREADS * (4 + c.window * c.window) + 15) & ~15;
@@ -2776,6 +3071,7 @@ struct be_ctx {
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
   bool step_lpe1;      // the one-lane-per-env fixed step kernel instead of step2_kernel (see below)
   int step5_lpe;       // W = 5: lanes per env of the fixed step kernel (1: be_kernel; 4 / 8: stepw_kernel)
+  int roll5_lpe;       // W = 5: lanes per env of the fused rollout (1: rollout_kernel; 4 / 8: rolloutw_kernel)
   int max_lds;         // the device's LDS bytes per workgroup
   int64_t blob_hdr[8]; // be_save_state's header (host memory that outlives the async copy)
   mutable struct { KFn fn; int lds; bool ok; } lds_cache[4];   // fits_lds() answers per (kernel, dynamic LDS)
@@ -2941,7 +3237,7 @@ const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
   switch (entry) {
     case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, !ctx->step_lpe1, ctx->step5_lpe); break;
     case BE_ENTRY_STEP_SAMPLED: L = pick_kernel(ctx->cfg, MODE_STEP, false); break;
-    case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok); if (!fits_lds(ctx, L)) L.fn = nullptr; break;
+    case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok, ctx->roll5_lpe); if (!fits_lds(ctx, L)) L.fn = nullptr; break;
     case BE_ENTRY_RESET: L = pick_kernel(ctx->cfg, MODE_RESET, false); break;
     case BE_ENTRY_OBSERVE: L = pick_kernel(ctx->cfg, MODE_OBSERVE, false); break;
     default: return nullptr;
@@ -3017,6 +3313,12 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   // W = 5 (BASELINE config 2): stepw_kernel's 8 lanes per env while one lane per env would leave
   // most of the chip idle (<= 64 envs per CU), the one-lane kernel above that.
   ctx->step5_lpe = (int64_t)cfg->num_envs <= (int64_t)64 * cus ? 8 : 1;
+  ctx->roll5_lpe = ctx->step5_lpe;
+  if (const char* l = getenv("BALLENV_ROLLOUT5_LPE")) {   // A/B override: "1", "4" or "8", else ignored
+    if (!strcmp(l, "1")) ctx->roll5_lpe = 1;
+    else if (!strcmp(l, "4")) ctx->roll5_lpe = 4;
+    else if (!strcmp(l, "8")) ctx->roll5_lpe = 8;
+  }
   if (const char* l = getenv("BALLENV_STEP5_LPE")) {   // A/B override: "1", "4" or "8", else ignored
     if (!strcmp(l, "1")) ctx->step5_lpe = 1;
     else if (!strcmp(l, "4")) ctx->step5_lpe = 4;
@@ -3171,14 +3473,14 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
   if (((uintptr_t)out->obs & 15) || (N * F) % 16)
     return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs a 16-byte aligned obs and num_envs * (4+W*W) % 16 == 0");
   if (steps == 0) return BE_OK;
-  const Launch L = pick_rollout(ctx->cfg, !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals);
+  const Launch L = pick_rollout(ctx->cfg, !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals, ctx->roll5_lpe);
   if (fits_lds(ctx, L)) {
     KParams a = make_params(ctx, st, out);
     a.actions = actions; a.steps = steps;
     int cur = -1;
     HIP_TRY(ctx, hipGetDevice(&cur));
     if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
-    const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
+    const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)L.threads);
     hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
     HIP_TRY(ctx, hipGetLastError());
     return BE_OK;

@@ -17,12 +17,15 @@ from test_gpu_parity import KEYS, make_env, np_state
 pytestmark = pytest.mark.gpu
 
 
-def _run_pair(cfg_py, N, W, K, chunks, seed=7, terminal=False):
+def _run_pair(cfg_py, N, W, K, chunks, seed=7, terminal=False, lens=None):
     """Env A: K be_step calls.  Env B: be_rollout over `chunks` (step counts summing to K)."""
     a, b = (make_env(cfg_py, N, W, "cuda:0", seed=seed, terminal_obs=terminal) for _ in range(2))
     acts = a.sample_actions(K, seed=seed + 1)
     a.reset()
     b.reset()
+    if lens is not None:   # random episode phases: goal changes and TimeLimit truncations early on
+        a.ep_len.copy_(lens)
+        b.ep_len.copy_(lens)
     F = 4 + W * W
     ref = {"obs": np.empty((K, N, F), np.uint8), "reward": np.empty((K, N)), "done": np.empty((K, N), bool),
            "truncated": np.empty((K, N), bool), "final_return": np.empty((K, N)), "final_len": np.empty((K, N), np.int32)}
@@ -238,3 +241,24 @@ def test_fused_rollouts_non_default_radius(gpu, r_obs):
     _run_pair(cfg, 4096, 10, 40, (15, 25), terminal=True)
     n_done, lit = _policy_pair(cfg, 4096, 10, 30, 30, True)
     assert lit > 0
+
+
+@pytest.mark.parametrize("N,tl,lpe,terminal", [(4096, 1000, "8", True), (4096, 20, "4", True), (1000, 7, "8", True),
+                                              (20000, 20, "8", False)])
+def test_rolloutw_matches_steps(gpu, N, tl, lpe, terminal, monkeypatch):
+    """rolloutw_kernel (W=5, 8 / 4 lanes per env, 32-env blocks; the small-batch fused rollout) ==
+    that many be_step calls of the one-lane step kernel, bit for bit -- per-step obs, reward, done,
+    truncated, final return / length, terminal obs, the state left behind and the stats slots
+    (folded every 32 steps in LDS) -- through mass truncation and partial blocks / waves, over
+    chunks that cross the 32-step fold window."""
+    from gym_ballenv_amd.config import EnvConfig
+    monkeypatch.setenv("BALLENV_ROLLOUT5_LPE", lpe)
+    monkeypatch.setenv("BALLENV_STEP5_LPE", "1")
+    e = make_env(EnvConfig(time_limit=tl), N, 5, gpu, seed=3)
+    assert e.kernel_name("rollout") == f"rolloutw_kernel<5, 13, 5, {lpe}>"
+    assert e.kernel_name("step") == "be_kernel<5, 0, 13, 5>"
+    e.close()
+    cfg = EnvConfig(time_limit=tl)
+    lens = torch.from_numpy(np.random.default_rng(N + tl).integers(0, tl, N).astype(np.int32)).to(gpu)
+    n_done = _run_pair(cfg, N, 5, 75, (1, 40, 34), terminal=terminal, lens=lens)
+    assert n_done > 0

@@ -19,8 +19,9 @@ ap.add_argument("--steps", type=int, default=1000)
 ap.add_argument("--settle", type=int, default=400)
 ap.add_argument("--var", default="")
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--rollout", action="store_true", help="time be_rollout (bench.py's fused leg) instead of be_step")
 a = ap.parse_args()
-var = a.var or ("BALLENV_STEP5_LPE" if a.window == 5 else "BALLENV_STEP_LPE")
+var = a.var or (("BALLENV_ROLLOUT5_LPE" if a.rollout else "BALLENV_STEP5_LPE") if a.window == 5 else "BALLENV_STEP_LPE")
 
 import torch  # noqa: E402
 import bench  # noqa: E402
@@ -32,7 +33,14 @@ for rep in range(a.reps):
     for n in [int(x) for x in a.envs.split(",")]:
         for l in a.lanes.split(","):
             os.environ[var] = l
-            r, k = bench.graph_steps_leg(gb, dev, 0, 1, stream, n, a.window, a.steps, a.settle)
+            if a.rollout:
+                args = argparse.Namespace(envs=n, window=a.window, rollout_steps=a.steps, rollout_chunk=100)
+                r = bench.rollout_leg(args, gb, dev, 0, 1, stream)
+                k = r["kernel"]
+                r["kernel_us_mean"] = r["kernel_us_per_step"]
+                r["roofline"] = {"frac": r["frac"]}
+            else:
+                r, k = bench.graph_steps_leg(gb, dev, 0, 1, stream, n, a.window, a.steps, a.settle)
             print(json.dumps({"rep": rep, "envs": n, "window": a.window, var: l, "kernel": k,
                               "kernel_us": round(r["kernel_us_mean"], 3), "value": r["value"],
                               "frac390": r["roofline"]["frac"]}), flush=True)
