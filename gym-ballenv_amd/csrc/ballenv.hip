@@ -2246,7 +2246,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
   __shared__ __align__(16) uint8_t s_stage[NWAVE][SW];
   __shared__ double s_fret[SC][32];              // finished envs' return / length per step of the fold window
   __shared__ int32_t s_flen[SC][32];
-  __shared__ uint8_t s_fdone[SC][NWAVE];         // per step and wave: its finished envs (bit g = env g of the wave)
+  __shared__ uint32_t s_fdone[SC][NWAVE];        // per step and wave: its finished envs (bit g = env g of the wave)
   constexpr int TW = (int)(sizeof(Tables) / 4);
 
   const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
@@ -2296,7 +2296,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
     for (int u = 0; u < n; ++u) {
       uint32_t m32 = 0u;
 #pragma unroll
-      for (int ww = 0; ww < NWAVE; ++ww) m32 |= (uint32_t)s_fdone[u][ww] << (ww * EPW);
+      for (int ww = 0; ww < NWAVE; ++ww) m32 |= s_fdone[u][ww] << (ww * EPW);
       if (m32 == 0u) continue;   // (uniform)
       const bool d = lane < 32 && ((m32 >> (lane & 31)) & 1u);
       const WaveStats ws = wave_stats(d, d ? s_fret[u][lane & 31] : 0.0, d ? s_flen[u][lane & 31] : 0);
@@ -2385,7 +2385,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
       uint32_t wm = 0u;
 #pragma unroll
       for (int g = 0; g < EPW; ++g) wm |= (uint32_t)((fm >> (g * L)) & 1ull) << g;
-      if (lane == 0) s_fdone[u][w] = (uint8_t)wm;
+      if (lane == 0) s_fdone[u][w] = wm;
     }
     // ---- autoreset: terminal obs, then the wave's resets (new obstacles through the LDS stash)
     const unsigned long long m = __ballot(valid && done && p.autoreset && h == 0);
