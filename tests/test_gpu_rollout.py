@@ -243,7 +243,7 @@ def test_fused_rollouts_non_default_radius(gpu, r_obs):
     assert lit > 0
 
 
-@pytest.mark.parametrize("N,tl,lpe,terminal", [(4096, 1000, "8", True), (4096, 20, "4", True), (1000, 7, "8", True),
+@pytest.mark.parametrize("N,tl,lpe,terminal", [(4096, 1000, "8", True), (4096, 20, "4", True), (1008, 7, "8", True),
                                               (20000, 20, "8", False)])
 def test_rolloutw_matches_steps(gpu, N, tl, lpe, terminal, monkeypatch):
     """rolloutw_kernel (W=5, 8 / 4 lanes per env, 32-env blocks; the small-batch fused rollout) ==
