@@ -1979,6 +1979,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   constexpr int TW = (int)(sizeof(Tables) / 4);
 
   if (DBG(DBG_EXIT_ENTRY)) return;
+  PH_INIT;
   const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
   const int el = tid / L, blk0 = (int)blockIdx.x * 32, i = blk0 + el, e0 = blk0 + w * EPW;
   const bool valid = i < N;
@@ -2023,6 +2024,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     return;
   }
   if (DBG(DBG_WAIT_LOADS)) __builtin_amdgcn_s_waitcnt(0);
+  PH(0);
 
   // ---- this lane's dynamic obstacles (ballenv_env.py:323-353): draws and moves need no action
   int counter = (int)((double)len0 * p.inv_g1);   // counter == ep_len mod (G+1)
@@ -2043,6 +2045,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     st_flags |= k < NDC ? fl : 0u;
     dnew[j] = pk(ox, oy);
   }
+  PH(1);
   // ---- action -> agent move + clamp (ballenv_env.py:247-259); unit moves and speeds
   st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
   const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
@@ -2054,6 +2057,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
   const double dist = calc_dist(gx, gy, ax, ay);
   const double rbase = (0.0 - p.time_penalty) + (old_dist - dist) / total;
+  PH(2);
 
   // ---- collision test, and the row masks of the obstacles that can light a cell
   //      (prep_state4 with quirk Q1, ball_cnn_ac3.py:384-412: row k is y offset k - W/2)
@@ -2079,6 +2083,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   word = lane_group_or<L>(word);
   const bool hs = (word >> 20) & 1u, hd = (word >> 21) & 1u;
   uint32_t rows = word & 0xFFFFFu;
+  PH(3);
 
   // ---- reward, done (ballenv_env.py:268-286, 200-229), on every lane of the group
   double reward = rbase;
@@ -2134,6 +2139,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
       }
     }
   }
+  PH(4);
   if (DBG(DBG_EXIT_PHYSICS)) return;
   const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && h == 0);
 
@@ -2180,6 +2186,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     }
   }
 
+  PH(5);
   // ---- observation (prep_state4): lane h writes bytes [BPL h, BPL (h+1)) of its env's row
   if (!DBG(DBG_NO_OBS)) {
     const int quad = quadrant(ax, ay, gx, gy);
@@ -2216,18 +2223,10 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     }
   }
 
+  PH(6);
+  PH_STORE;
 }
 
-// rolloutw_kernel<5, NS, ND, L>: be_rollout (p.steps consecutive steps in one launch, each env's
-// state in registers) with L lanes per env and 32-env blocks, for small batches at W=5 (BASELINE
-// config 2's 4 096 envs: the one-lane rollout_kernel runs them on 16 blocks).  The per-step body
-// is stepw_kernel's (obstacle slots k = L j + h per lane, one packed row word OR-ed over the group,
-// the per-env chains on every lane of the group, wave_resets with the owner at h = 0); the state
-// stays in registers as in rollout_kernel -- each lane holds only its own obstacles, a reset's new
-// positions reach them through a per-wave LDS stash.  Outputs are per step, in (steps, N, ...)
-// rows.  Stats: the block's 32 envs share a slot; every wave records its finished envs of each
-// step in LDS and every SC steps (and at the end) wave 0 folds them step by step, each step's in
-// env order -- rollout_kernel's per-half-wave, per-step sums, bit for bit.
 template <int WT, int NSC, int NDC, int L>
 __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
   constexpr int CT = 32 * L, EPW = 64 / L, NWAVE = CT / 64, G = NSC + NDC;
@@ -2305,6 +2304,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
     }
   };
 
+  PH_INIT;
   for (int s = 0; s < p.steps; ++s) {
     const size_t so_n = (size_t)s * N;
     // next step's action: in flight while this step runs
@@ -2326,6 +2326,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
       st_flags |= k < NDC ? fl : 0u;
       dp[j] = pk(ox, oy);
     }
+    PH(0);
     // ---- action -> agent move + clamp (ballenv_env.py:247-259)
     st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
     const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
@@ -2334,6 +2335,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
     const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
     const double dist = calc_dist(gx, gy, ax, ay);
     const double rbase = (0.0 - p.time_penalty) + (old_dist - dist) / total;
+    PH(1);
     // ---- collision test and row masks (stepw_kernel's)
     uint32_t word = 0u;
     auto obstacle = [&](int32_t opk, bool real, uint32_t hit_bit) {
@@ -2357,6 +2359,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
     word = lane_group_or<L>(word);
     const bool hs = (word >> 20) & 1u, hd = (word >> 21) & 1u;
     uint32_t rows = word & 0xFFFFFu;
+    PH(2);
     // ---- reward, done (ballenv_env.py:268-286, 200-229)
     double reward = rbase;
     if (hs) reward -= p.static_penalty;          // statics come first in obstacle_list (Q3)
@@ -2387,6 +2390,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
       for (int g = 0; g < EPW; ++g) wm |= (uint32_t)((fm >> (g * L)) & 1ull) << g;
       if (lane == 0) s_fdone[u][w] = wm;
     }
+    PH(3);
     // ---- autoreset: terminal obs, then the wave's resets (new obstacles through the LDS stash)
     const unsigned long long m = __ballot(valid && done && p.autoreset && h == 0);
     if (m) {
@@ -2422,6 +2426,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
         for (int k = 0; k < KR; ++k) rows |= xrows[k] << (WT * k);
       }
     }
+    PH(4);
     // ---- observation (prep_state4) into the wave's stage, its 64/L rows out
     if (p.obs) {
       const int quad = quadrant(ax, ay, px(goal), py(goal));
@@ -2457,13 +2462,16 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    PH(5);
     if (slot && (u == SC - 1 || s + 1 == p.steps)) {   // (uniform: every wave runs every step)
       __syncthreads();
       fold(u + 1);
       __syncthreads();   // the window's LDS is free again
     }
     a = a_next;
+    PH(6);
   }
+  PH_STORE;
 
   // ---- state back to HBM, once
   if (valid) {
