@@ -2304,6 +2304,14 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
     }
   };
 
+  // the obstacles' goal-change counter (== ep_len mod (G+1)) kept incrementally, and each step's
+  // Philox block computed one step ahead: the next step's (episode, ep_len + 1) block runs beside
+  // this step's work, off its critical path (recomputed after a reset for the envs that reset)
+  int counter = (int)((double)len * p.inv_g1);
+  counter = len - counter * (p.goal_change + 1);
+  if (counter < 0) counter += p.goal_change + 1;
+  if (counter > p.goal_change) counter -= p.goal_change + 1;
+  u4 bnext = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 0u), p.seed);
   PH_INIT;
   for (int s = 0; s < p.steps; ++s) {
     const size_t so_n = (size_t)s * N;
@@ -2311,12 +2319,10 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
     const int a_next = s + 1 < p.steps ? ld_s(p.actions + so_n + N, ic) : 0;
     const int gx = px(goal), gy = py(goal);
     // ---- this lane's dynamic obstacles (ballenv_env.py:323-353)
-    int counter = (int)((double)len * p.inv_g1);   // counter == ep_len mod (G+1)
-    counter = len - counter * (p.goal_change + 1);
-    if (counter < 0) counter += p.goal_change + 1;
-    if (counter > p.goal_change) counter -= p.goal_change + 1;
     const bool change = counter >= p.goal_change;
-    const u4 b0 = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+    counter = change ? 0 : counter + 1;
+    const u4 b0 = bnext;
+    bnext = philox(gid, episode, (uint32_t)(len + 1), tag(PURPOSE_STEP_OBS, 0u), p.seed);
 #pragma unroll
     for (int j = 0; j < SD; ++j) {
       const int k = L * j + h;
@@ -2405,10 +2411,11 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
       int gxr = gx, gyr = gy;
       int32_t* ost = &s_ost[w][0];
       auto osink = [&](int sl, int k, int, int32_t o) { ost[sl * G + k] = o; };
+      bool reset_now = false;
       auto esink = [&](int own, int32_t ag, int32_t go, int32_t a0) {   // every lane of the env's group
         goal = go;
         total = reset_dists(ag, go, a0, old_dist);
-        ret = 0.0; len = 0; ++episode; was_reset = true;
+        ret = 0.0; len = 0; ++episode; was_reset = true; reset_now = true; counter = 0;
 #pragma unroll
         for (int j = 0; j < SS; ++j) so[j] = ost[own * G + min(L * j + h, NSC - 1)];
 #pragma unroll
@@ -2425,6 +2432,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
 #pragma unroll
         for (int k = 0; k < KR; ++k) rows |= xrows[k] << (WT * k);
       }
+      if (reset_now) bnext = philox(gid, episode, 0u, tag(PURPOSE_STEP_OBS, 0u), p.seed);
     }
     PH(4);
     // ---- observation (prep_state4) into the wave's stage, its 64/L rows out
