@@ -2625,15 +2625,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   const v2s boxo = {(short)bxo, (short)byo};
   const v2u boxw = {(unsigned short)nb0.bw, (unsigned short)nb0.bh};
 
-  // the obstacles' goal-change counter (== ep_len mod (G+1)) kept incrementally; each step's Philox
-  // block (and the policy's uniform) computed one step ahead, beside the current step's work
-  // (recomputed after a reset for the envs that reset)
-  int counter = (int)((double)len * p.inv_g1);
-  counter = len - counter * (p.goal_change + 1);
-  if (counter < 0) counter += p.goal_change + 1;
-  if (counter > p.goal_change) counter -= p.goal_change + 1;
-  u4 bnext = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 0u), p.seed);
-  float unext = POL ? policy_uniform(gid, episode, (uint32_t)len, p.pol_seed) : 0.f;
   PH_INIT;
   for (int s = 0; s < p.steps; ++s) {
     const size_t so_n = (size_t)s * N;
@@ -2648,9 +2639,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       float* lg = reinterpret_cast<float*>(pimg + PL.logits);
       if (DBG(DBG_POL_TABLE)) pnz = false;
       const int c3 = s % 3;
-      // the draw's uniform, a function of this env's state (computed one step ahead)
-      const float u = unext;
-      unext = policy_uniform(gid, episode, (uint32_t)(len + 1), p.pol_seed);
+      // the draw's uniform, a function of this env's state (in flight across the barrier)
+      const float u = policy_uniform(gid, episode, (uint32_t)len, p.pol_seed);
       int my_k = 0;   // this env's place in the list
       if (valid && pnz) {
         my_k = atomicAdd(&cnt3[c3], 1);
@@ -2788,10 +2778,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     bool hs = false, hd = false;
     nl.cnt = 0;
     // ---- dynamic obstacles (counter == ep_len mod (G+1): all start at 0 on reset)
+    int counter = (int)((double)len * p.inv_g1);
+    counter = len - counter * (p.goal_change + 1);
+    if (counter < 0) counter += p.goal_change + 1;
+    if (counter > p.goal_change) counter -= p.goal_change + 1;
     const bool change = counter >= p.goal_change;
-    counter = change ? 0 : counter + 1;
-    const u4 b0 = bnext;
-    bnext = philox(gid, episode, (uint32_t)(len + 1), tag(PURPOSE_STEP_OBS, 0u), p.seed);
+    const u4 b0 = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 0u), p.seed);
     u4 b1{0u, 0u, 0u, 0u};
     if (NDC > 5) b1 = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 1u), p.seed);
     const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
@@ -2863,11 +2855,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       }
       int32_t* ost = &s_ost[w][0];
       auto osink = [&](int sl, int k, int, int32_t o) { ost[sl * G + k] = o; };
-      bool reset_now = false;
       auto esink = [&](int own, int32_t ag, int32_t go, int32_t a0) {
         goal = go;
         total = reset_dists(ag, go, a0, old_dist);
-        ret = 0.0; len = 0; ++episode; was_reset = true; reset_now = true; counter = 0;
+        ret = 0.0; len = 0; ++episode; was_reset = true;
 #pragma unroll
         for (int k = 0; k < NSC; ++k) so[k] = ost[own * G + k];
 #pragma unroll
@@ -2877,10 +2868,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
         wave_resets<WT, NSC, NDC, 1>(p, t, m, i, gid, episode, ax, ay, gxr, gyr, nl.cnt, xrows, &s_rows[w][0], osink, esink);
       else
         wave_resets<WT, NSC, NDC, 64>(p, t, m, i, gid, episode, ax, ay, gxr, gyr, nl.cnt, xrows, &s_rows[w][0], osink, esink);
-      if (reset_now) {
-        bnext = philox(gid, episode, 0u, tag(PURPOSE_STEP_OBS, 0u), p.seed);
-        if constexpr (POL) unext = policy_uniform(gid, episode, 0u, p.pol_seed);
-      }
     }
 
     PH(6);
