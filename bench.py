@@ -37,6 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+DIST_ON = False         # a torch.distributed process group is up (any launch under torchrun, even 1 rank)
 
 
 def parse():
@@ -159,7 +160,7 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
     import torch
     import torch.distributed as dist
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0.record(stream)
@@ -169,9 +170,9 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
-    if world > 1:
+    if DIST_ON:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -264,7 +265,7 @@ def policy_leg(args, gb, dev, rank, world, stream):
     ro_chunk, img_bytes = ro.chunk, ro.hp.packed_bytes
     ro.run()                                         # warm-up horizon
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if DIST_ON:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -273,10 +274,10 @@ def policy_leg(args, gb, dev, rank, world, stream):
     ro.run()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if DIST_ON:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -387,7 +388,7 @@ def rollout_leg(args, gb, dev, rank, world, stream):
     a0 = acts.data_ptr()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     sp = C.c_void_p(stream.cuda_stream)
-    if world > 1:
+    if DIST_ON:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -399,10 +400,10 @@ def rollout_leg(args, gb, dev, rank, world, stream):
             _abi.check(rc, ctx)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if DIST_ON:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -596,7 +597,7 @@ def board_leg(args, gb, dev, rank, world, stream):
     f, r, dn, info = b.rollout(acts[:Kc])
     out = gb._abi.BeBoardOut(f.data_ptr(), r.data_ptr(), dn.data_ptr(), info["truncated"].data_ptr())
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if DIST_ON:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -607,10 +608,10 @@ def board_leg(args, gb, dev, rank, world, stream):
         lib.be_board_rollout(b._h, C.byref(b._st), C.c_void_p(acts[c0].data_ptr()), None, Kc, C.byref(out), sp)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if DIST_ON:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -634,9 +635,11 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
+    global DIST_ON
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    DIST_ON = "WORLD_SIZE" in os.environ   # under torchrun: the collectives run even at one rank
     if args.gpus != world:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU: "
                          f"torchrun --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}, or bench.py --gpus N alone)")
@@ -654,7 +657,7 @@ def main():
         local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    if DIST_ON:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -730,7 +733,7 @@ def main():
         torch.cuda.synchronize(dev)
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0.record(stream)
@@ -748,10 +751,10 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize(dev)   # (measured: a spin on the end event first adds ~1.5 us, tools/sync_cost.py)
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     n_devices = 1
-    if world > 1:
+    if DIST_ON:
         el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
@@ -827,7 +830,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     env.close()
-    if world > 1:
+    if DIST_ON:
         dist.destroy_process_group()
 
 

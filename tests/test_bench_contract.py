@@ -87,3 +87,27 @@ def test_bench_multi_rank_gloo(gpu):
     assert e2["min_return"] == e1["min_return"] and e2["max_return"] == e1["max_return"]
     assert e2["mean_return"] == pytest.approx(e1["mean_return"], rel=1e-12)
     assert e2["mean_length"] == pytest.approx(e1["mean_length"], rel=1e-12)
+
+
+@pytest.mark.gpu
+def test_bench_rccl_one_rank(gpu):
+    """The RCCL path of bench.py (the driver's torchrun form, backend nccl = RCCL): under
+    torch.distributed.run with one rank the process group comes up and every collective of the
+    timed regions runs (barriers, the max-over-ranks all_reduce, the stats all_gather, the device
+    all_gather_object) -- the multi-GPU code path minus the other ranks, which one GPU cannot host."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr=127.0.0.1",
+           f"--master-port={port}", "bench.py", "--gpus", "1", "--dist-backend", "nccl", "--steps", "20", "--warmup", "5",
+           "--settle", "60", "--rollout-steps", "100", "--policy-steps", "20", "--torch-policy-steps", "0",
+           "--board-steps", "20", "--cold-steps", "0", "--config2-steps", "20", "--large-steps", "0",
+           "--from-reset-steps", "0", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["ranks"] == 1 and d["n_gpus"] == 1 and d["value"] > 0 and d["episodes"]["episodes"] >= 0
+    for leg in ("policy_rollout", "fused_rollout", "board_profile", "config2"):
+        assert d[leg]["value"] > 0, leg
