@@ -136,14 +136,22 @@ __device__ void features(const BParams& p, int64_t row, double ax, double ay, do
 #pragma unroll
   for (int k = 0; k < 20; ++k) f[k] = 0.f;
   // calcDistanceFromGoal (:132-144): floor(hypot / 5), capped at 5
+#ifdef BE_BOARD_DIAG_NOHYPOT   // diagnostics (timing placebo, wrong features)
+  const double dg = floor((fabs(ax - gx) + fabs(ay - gy)) / 5.0);
+#else
   const double dg = floor(hypot(ax - gx, ay - gy) / 5.0);
+#endif
   f[0] = (float)(dg > 5.0 ? 5.0 : dg);
   // relativeGoalPos (:146-166): angle between (0, 1) and (gx - ax, gy - ay)
   const double vx = gx - ax, vy = gy - ay;
   const double nv = sqrt(__dadd_rn(__dmul_rn(vx, vx), __dmul_rn(vy, vy)));
   double c = nv > 0.0 ? vy / nv : 0.0;
   c = c < -1.0 ? -1.0 : (c > 1.0 ? 1.0 : c);
+#ifdef BE_BOARD_DIAG_NOACOS    // diagnostics (timing placebo, wrong features)
+  const double ang = 1.5 - c;
+#else
   const double ang = acos(c);
+#endif
   if (ang < PI / 4) f[1] = 1.f;
   else if (ang > PI / 4 && ang < PI * 3 / 4) { if (vx > 0) f[2] = 1.f; else f[4] = 1.f; }
   else f[3] = 1.f;
@@ -162,7 +170,11 @@ __device__ void features(const BParams& p, int64_t row, double ax, double ay, do
     c11 += real ? 1.f : 0.f;                               // orientation bin 1, speed bin 0
     // a*exp(-N/b)*N*thrPart, a = 1, b = 10; -N*0.1 is within an ulp of -N/10 (exp's own
     // accuracy class; only sf's f32 value and its > 1 cut, a measure-zero boundary, see it)
+#ifdef BE_BOARD_DIAG_NOEXP     // diagnostics (timing placebo, wrong features)
+    const double fsoc = (1.0 - N * 0.1) * N * 1.5;
+#else
     const double fsoc = exp(N * -0.1) * N * 1.5;
+#endif
     tk[j] = (real && fsoc > 1.0) ? fsoc : 0.0;             // -> phi_SF[orientation bin 1]
   }
   double sf = 0.0;
