@@ -129,7 +129,7 @@ __device__ __forceinline__ double pair_lead_f64(double v) {    // the pair's lan
 // The pair's counts are exact small integers; the social-force sum adds the per-obstacle terms in
 // the reference's obstacle order on both lanes.  Lane h writes the row's float4 words h, h+L, ...
 template <int MAXS, int L>
-__device__ void features(const BParams& p, int64_t row, double ax, double ay, double gx, double gy,
+__device__ void features(const BParams& p, float4* out, double ax, double ay, double gx, double gy,
                          const double (&dk)[(MAXS + L - 1) / L], int h) {
   constexpr int SPL = (MAXS + L - 1) / L;
   float f[20];
@@ -195,7 +195,7 @@ __device__ void features(const BParams& p, int64_t row, double ax, double ay, do
   }
   f[5] = c5; f[6] = c6; f[7] = c7; f[8 + 3 * 1 + 0] = c11;
   f[17 + 1] = (float)sf;
-  float4* out = reinterpret_cast<float4*>(p.features + row * 20);   // 80-B rows: 5 x 16 B
+  // out: this env's 80-B row (5 x 16 B) in the wave's LDS stage (board_kernel copies the rows out)
 #pragma unroll
   for (int k = 0; k < 5; ++k)
     if (k % L == h) out[k] = make_float4(f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
@@ -402,9 +402,38 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
 // terms of obstacles k = L j + h (the pair combines them, above), the per-env chains (distance,
 // reward, the goal features) run on both lanes, and the pair splits the stores.  Two lanes give
 // two waves per SIMD at 65 536 envs where one lane per env leaves one.
+// A wave's feature rows (EPW x 80 B, contiguous in the output) from its LDS stage to HBM with
+// 16-byte stores in lane order: whole cache lines per store instruction, where a lane's own row
+// would scatter 5 stores over 64 rows at an 80-B stride.
+template <int EPW>
+__device__ __forceinline__ void copy_feat(const float4* stage, float* dst, int nrows, int lane) {
+  const int nv = nrows * 5;
+  float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll
+  for (int j = 0; j < (EPW * 5 + 63) / 64; ++j) {
+    const int v = lane + 64 * j;
+    if (v < nv) d4[v] = stage[v];
+  }
+}
+
 template <int MAXS, bool ROLL, int L>
 __global__ __launch_bounds__(256) void board_kernel(BParams p) {
-  constexpr int SPL = (MAXS + L - 1) / L;
+  constexpr int SPL = (MAXS + L - 1) / L, EPW = 64 / L;
+  __shared__ float4 s_feat[4][EPW * 5];   // per wave: its envs' feature rows
+  const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+  float4* fstage = &s_feat[w][0];
+  float4* frow = fstage + (lane / L) * 5;
+  const int e0 = (int)blockIdx.x * (256 / L) + w * EPW;          // the wave's first env
+  const int nrows = max(0, min(EPW, p.n - e0));
+  auto feat_out = [&](int64_t row0) {   // the wave's staged rows to features[row0 ..]
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    copy_feat<EPW>(fstage, p.features + row0 * 20, nrows, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the next step's stage writes follow
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
   // every lane of a wave stays to the end (the Philox resets are wave-cooperative); lanes past
   // N work on a clamped index and store nothing
   const int h = (int)(threadIdx.x & (L - 1));
@@ -427,7 +456,8 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   };
   if (p.mode == 2) {
     obstacle_dists();
-    if (valid) features<MAXS, L>(p, i, ax, ay, gx, gy, dk, h);
+    if (valid) features<MAXS, L>(p, frow, ax, ay, gx, gy, dk, h);
+    feat_out(e0);
     return;
   }
   uint32_t episode = p.episode[i];
@@ -514,9 +544,12 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       fresh = true;
       obstacle_dists();
     }
-    if (valid && p.features) {
-      if (!moved) obstacle_dists();
-      features<MAXS, L>(p, row, ax, ay, gx, gy, dk, h);
+    if (p.features) {   // (uniform)
+      if (valid) {
+        if (!moved) obstacle_dists();
+        features<MAXS, L>(p, frow, ax, ay, gx, gy, dk, h);
+      }
+      feat_out((int64_t)s * p.n + e0);
     }
   }
   if (!valid) return;

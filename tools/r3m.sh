@@ -1,0 +1,6 @@
+set -u
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_board.py > gpurun_out/r3m_pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/r3m_pytest.log; [ $rc -ne 0 ] && { grep -E "^E " gpurun_out/r3m_pytest.log | head; exit $rc; }
+B=boardold bash tools/board_ab.sh
