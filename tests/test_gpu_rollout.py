@@ -228,6 +228,23 @@ def test_policy_rollout_crowded_multi_round(gpu):
 
 
 @pytest.mark.parametrize("r_obs", [21, 58])
+def test_w5_small_batch_kernels_non_default_radius(gpu, r_obs, monkeypatch):
+    """stepw_kernel / rolloutw_kernel (W=5, eight lanes per env) at a larger collision radius
+    (R = 26 / 63: wider near boxes, more lit cells and collisions) against the one-lane kernels."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg = EnvConfig(radius_obstacle=r_obs, time_limit=30)
+    monkeypatch.setenv("BALLENV_STEP5_LPE", "1")
+    monkeypatch.setenv("BALLENV_ROLLOUT5_LPE", "8")
+    e = make_env(cfg, 4096, 5, gpu, seed=3)
+    assert e.kernel_name("rollout") == "rolloutw_kernel<5, 13, 5, 8>" and e.kernel_name("step") == "be_kernel<5, 0, 13, 5>"
+    e.close()
+    _run_pair(cfg, 4096, 5, 40, (15, 25), terminal=True)            # rolloutw vs one-lane steps
+    monkeypatch.setenv("BALLENV_STEP5_LPE", "8")
+    monkeypatch.setenv("BALLENV_ROLLOUT5_LPE", "1")
+    _run_pair(cfg, 4096, 5, 40, (40,), terminal=True)                # one-lane rollout vs stepw steps
+
+
+@pytest.mark.parametrize("r_obs", [21, 58])
 def test_fused_rollouts_non_default_radius(gpu, r_obs):
     """A larger collision radius R = radius_obstacle + radius_agent grows the fused kernels' LDS
     (near lists, row-span table).  At R >= 26 the config-5 kernel no longer fits the CU's 160 KB,
