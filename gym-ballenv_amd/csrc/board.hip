@@ -49,6 +49,24 @@
 namespace {
 
 constexpr uint32_t PURPOSE_BOARD_RESET = 6;
+
+// Diagnostics-only build (-DBE_DIAG_STAMPS): per-wave cycles per phase (s_memtime deltas summed over
+// a launch), read with be_board_diag_stamps; BPH(k) closes phase k.
+#ifdef BE_DIAG_STAMPS
+constexpr int BDIAG_WAVES = 1 << 14;
+__device__ unsigned long long g_bdiag[BDIAG_WAVES][8];
+#define BPH_INIT unsigned long long bph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bph_t = __builtin_amdgcn_s_memtime()
+#define BPH(k) do { const unsigned long long bph_n = __builtin_amdgcn_s_memtime(); bph_acc[k] += bph_n - bph_t; bph_t = bph_n; } while (0)
+#define BPH_STORE do { \
+    const int bph_w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64); \
+    if ((threadIdx.x & 63) == 0 && bph_w < BDIAG_WAVES) \
+      for (int bph_k = 0; bph_k < 8; ++bph_k) g_bdiag[bph_w][bph_k] = bph_acc[bph_k]; \
+  } while (0)
+#else
+#define BPH_INIT ((void)0)
+#define BPH(k) ((void)0)
+#define BPH_STORE ((void)0)
+#endif
 constexpr int BOARD_REJECT_LIMIT = 4096;
 constexpr double PI = 3.141592653589793;   // math.pi
 
@@ -460,6 +478,7 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     feat_out(e0);
     return;
   }
+  BPH_INIT;
   uint32_t episode = p.episode[i];
   double total = p.total[i], ret = p.ep_return[i], dist = p.dist[i];
   int32_t len = p.ep_len[i];
@@ -481,6 +500,7 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       } else {
         dx = p.deltas[2 * row]; dy = p.deltas[2 * row + 1];
       }
+      BPH(0);
       // self.old_dist (:652) = |agent - goal|, which the previous step of this launch left in dist
       const double old = fresh ? dist2(ax, ay, gx, gy) : dist;
       double nx = ax + dx, ny = ay + dy;
@@ -512,6 +532,7 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
         if (h == L - 1 && p.truncated) p.truncated[row] = trunc ? 1 : 0;
       }
       do_reset = valid && done && p.autoreset;
+      BPH(1);
     }
     if (p.tape) {   // parity mode: the reference's draw order, on the env's own lane(s)
       if (do_reset) reset_env(p, i, episode + 1u, ax, ay, gx, gy, dist, total, so);
@@ -544,14 +565,18 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       fresh = true;
       obstacle_dists();
     }
+    BPH(2);
     if (p.features) {   // (uniform)
       if (valid) {
         if (!moved) obstacle_dists();
         features<MAXS, L>(p, frow, ax, ay, gx, gy, dk, h);
       }
+      BPH(3);
       feat_out((int64_t)s * p.n + e0);
+      BPH(4);
     }
   }
+  BPH_STORE;
   if (!valid) return;
   if (was_reset && h == L - 1) {
 #pragma unroll
@@ -733,6 +758,13 @@ int be_board_rollout(be_board* b, const be_board_state* st, const uint8_t* actio
 int be_board_observe(be_board* b, const be_board_state* st, const be_board_out* out, void* stream) {
   return board_launch(b, st, out, 2, nullptr, nullptr, nullptr, nullptr, 0, stream);
 }
+
+#ifdef BE_DIAG_STAMPS
+// diagnostics build only: the per-wave phase cycles of the last board launch (BDIAG_WAVES x 8)
+int be_board_diag_stamps(unsigned long long* cy) {
+  return hipMemcpyFromSymbol(cy, HIP_SYMBOL(g_bdiag), sizeof(g_bdiag)) == hipSuccess ? BE_OK : BE_E_HIP;
+}
+#endif
 
 int be_board_status(be_board* b, int32_t* status_out, void* stream) {
   if (!b || !status_out) return bfail(b, BE_E_INVALID, "bad arguments to be_board_status");
