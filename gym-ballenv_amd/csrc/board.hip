@@ -311,21 +311,15 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
       u = slot == s2 ? u2 : u; ep = slot == s2 ? e2 : ep;
     }
     const bool act = slot < n;
-    // the three Philox chains of a pass's first round -- the goal, this lane's agent attempt, this
-    // lane's static attempt -- are independent of each other's values: issued together they
-    // overlap (the rejection logic below depends on goal -> agent -> statics)
-    const u4 bg = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, 0u), p.seed);
-    const u4 ba0 = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (1u << 20) | (uint32_t)sl), p.seed);
-    const u4 bo0 = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (2u << 20) | ((uint32_t)k_l << 12) | (uint32_t)a_l), p.seed);
     // goal (ballenv_pygame.py:462-463), on every lane of the slot
+    const u4 bg = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, 0u), p.seed);
     const double rgx = (double)(p.W - p.sgx) + ranf2(bg.x, bg.y) * (double)p.sgx;
     const double rgy = (double)(p.H - p.sgy) + ranf2(bg.z, bg.w) * (double)p.sgy;
     // agent attempts r0 + sl (:464-481)
     double rax = 0.0, ray = 0.0, rd0 = 0.0;
     unsigned open = (1u << n) - 1u;
     for (int r0 = 0; open; r0 += LS) {
-      u4 ba = ba0;
-      if (r0 > 0) ba = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (1u << 20) | (uint32_t)(r0 + sl)), p.seed);
+      const u4 ba = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (1u << 20) | (uint32_t)(r0 + sl)), p.seed);
       const double cx = ranf2(ba.x, ba.y) * (double)p.sax, cy = ranf2(ba.z, ba.w) * (double)p.say;
       const double dc = dist2(rgx, rgy, cx, cy);
       if (r0 == 0) {
@@ -369,8 +363,7 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
       bool ok = false;
       int32_t cand = 0;
       if (act && ns > 0 && a_l < per && a < st_end && ((mine >> k_l) & 1ull)) {
-        u4 bo = bo0;
-        if (a0 > 0) bo = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (2u << 20) | ((uint32_t)k_l << 12) | (uint32_t)a), p.seed);
+        const u4 bo = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (2u << 20) | ((uint32_t)k_l << 12) | (uint32_t)a), p.seed);
         const int ox = p.sox + (int)__umulhi(bo.x, (uint32_t)(p.W - 2 * p.sox));
         const int oy = p.soy + (int)__umulhi(bo.y, (uint32_t)(p.H - 2 * p.soy));
         ok = dist2((double)ox, (double)oy, rax, ray) - p.thr_agent > p.r_collide &&
