@@ -25,7 +25,11 @@ OUT = os.path.join(PKG, "libballenv.so")
 ARCH = os.environ.get("BALLENV_OFFLOAD_ARCH", "gfx950")
 
 BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}"]
-UNITS = {"ballenv.hip": [], "policy.hip": ["-fno-slp-vectorize"], "features.hip": [], "board.hip": []}
+# -amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs.  The compiler's default put the fc1
+# tiles' accumulators in AGPRs, which costs 12 v_accvgpr_read per tile row (of ~70 VALU); only
+# the kernels with MFMAs (the policy forward and the fused policy rollouts) change.
+VGPR_MFMA = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+UNITS = {"ballenv.hip": VGPR_MFMA, "policy.hip": ["-fno-slp-vectorize", *VGPR_MFMA], "features.hip": [], "board.hip": []}
 HEADERS = [HDR, os.path.join(CSRC, "philox.h"), os.path.join(CSRC, "internal.h"), os.path.join(CSRC, "policy_core.h")]
 
 

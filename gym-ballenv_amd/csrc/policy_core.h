@@ -75,6 +75,17 @@ __device__ __forceinline__ uint32_t or_groups(uint32_t x) {
   return b[0] | b[1];
 }
 
+// fc1 pre-activation from its three digit-plane accumulators: hi * 2^16 + mid * 2^8 + lo (mod 2^32),
+// as (((hi << 8) + mid) << 8) + lo: two v_lshl_add_u32.  The empty asm keeps the inner sum from
+// being re-associated into the compiler's form (two shifts and an add3, one VALU instruction more
+// per element); the instructions themselves stay the compiler's, so it still inserts the wait
+// states a VALU read of an MFMA result needs.
+__device__ __forceinline__ int digits(int hi, int mid, int lo) {
+  uint32_t t = ((uint32_t)hi << 8) + (uint32_t)mid;
+  asm("" : "+v"(t));
+  return (int)((t << 8) + (uint32_t)lo);
+}
+
 // Hidden rows are summed in 4 fixed chunks of 16-row tiles, chunk c = [c*HT/4, (c+1)*HT/4):
 // logit = ((s_0 + s_1) + s_2) + s_3 with s_c the chunk's FMA chain summed over the lane groups.
 // One wave can run all four (tile_forward) or four waves one each (the fused rollout kernel),
@@ -117,7 +128,7 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
     float h[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int q = (int)(((uint32_t)acc[0][r] << 16) + ((uint32_t)acc[1][r] << 8)) + acc[2][r];
+      const int q = digits(acc[0][r], acc[1][r], acc[2][r]);
       h[r] = (float)(q > 0 ? q : 0);
     }
     if (!(dbg & 4)) {
@@ -168,8 +179,8 @@ __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[
     float h0[4], h1[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int q0 = (int)(((uint32_t)a0[0][r] << 16) + ((uint32_t)a0[1][r] << 8)) + a0[2][r];
-      const int q1 = (int)(((uint32_t)a1[0][r] << 16) + ((uint32_t)a1[1][r] << 8)) + a1[2][r];
+      const int q0 = digits(a0[0][r], a0[1][r], a0[2][r]);
+      const int q1 = digits(a1[0][r], a1[1][r], a1[2][r]);
       h0[r] = (float)(q0 > 0 ? q0 : 0);
       h1[r] = (float)(q1 > 0 ? q1 : 0);
     }
