@@ -353,7 +353,7 @@ def policy_roofline(args, gb, dev, rank, pol, us_per_step, chunk, img):
                       "blocks are one block per CU, and the 89-KB policy image leaves LDS for only one): env "
                       "physics, select_action's softmax/draw and the head FMAs of the dense tiles"}
     # counters of the same kernel / envs / chunk (tools/pmc_passes.sh + tools/pmc_report.py, committed profile)
-    pmc = os.path.join(ROOT, "profiles", "r02_pmc_policy_rollout.json")
+    pmc = os.path.join(ROOT, "profiles", "r03_pmc_policy_rollout.json")
     if os.path.exists(pmc):
         d = json.load(open(pmc))
         if d.get("units_per_dispatch") == N * chunk and f"rollout_kernel<{W}, 13, 5, {HT}, {KS}," in (d.get("kernel") or ""):
@@ -589,7 +589,7 @@ def board_leg(args, gb, dev, rank, world, stream):
                        "random actionArray moves, autoreset, hipGraph replay",
            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
            "kernel_us_mean": ms * 1e3, "bytes_per_env_step": B, "achieved_GBs": B * N / (ms * 1e-3) / 1e9}
-    res["roofline"] = board_roofline(B, N, ms * 1e3, committed_pmc("r02_pmc_board_step.json", "board_kernel<6, false>", N))
+    res["roofline"] = board_roofline(B, N, ms * 1e3, committed_pmc("r03_pmc_board_step.json", "board_kernel<6, false", N))
     del g
     # the same rollout fused: be_board_rollout, 100 steps per launch with the state in registers
     Kc = min(100, T)
@@ -625,7 +625,7 @@ def board_leg(args, gb, dev, rank, world, stream):
     Bf = 1 + 8 + 2 + 80 + (2 * 44 + 28 + 24) / Kc
     res["fused"]["bytes_per_env_step"] = Bf
     res["fused"]["roofline"] = board_roofline(Bf, N, res["fused"]["kernel_us_per_step"],
-                                              committed_pmc("r02_pmc_board_rollout.json", "board_kernel<6, true>",
+                                              committed_pmc("r03_pmc_board_rollout.json", "board_kernel<6, true",
                                                             N * Kc))
     b.close()
     return res
