@@ -293,6 +293,10 @@ int be_policy_create(be_ctx* ctx, int32_t hidden, int32_t num_actions, be_policy
   if (!pol) return be_ctx_fail(ctx, BE_E_NOMEM, "out of host memory");
   pol->ctx = ctx; pol->cv = cv; pol->H = hidden; pol->F = F; pol->A = num_actions;
   pol->k = pick_policy(hidden, F, num_actions);
+  if (pol_unpadded(pol->k.NO) && pol->k.NO != num_actions + 1) {   // the kernels' compile-time A
+    delete pol;
+    return be_ctx_fail(ctx, BE_E_INVALID, "policy layout / action count mismatch");
+  }
   if (const char* d = getenv("BALLENV_POLICY_DEBUG")) pol->dbg = (int)strtoul(d, nullptr, 0);
   pol->L = pol_layout(pol->k.HT, pol->k.KS, pol->k.NO);
   if (pol->L.lds > 160 * 1024) {

@@ -214,6 +214,11 @@ __device__ __forceinline__ void tile_forward(const uint8_t* lds, const v4i (&B)[
 // policy_pick draws by inverse CDF of u.  policy_finish is both, with u from
 // Philox(seed; gid, episode, ep_len, POLICY).  An env on the empty-window table has one of 4
 // distributions, which the fused rollout computes once per launch -- same ops, same result.
+// pick_policy builds the NO = 10 layouts only for A = 9 actions (NO = A + 1: no pad outputs); the
+// generic NO = 16 layout pads with -inf logits.  With no pads every `o < A` test below is true at
+// compile time (a runtime A kept nine loop-invariant lane masks live in spilled SGPRs).
+__host__ __device__ constexpr bool pol_unpadded(int NO) { return NO == 10; }
+
 template <int NO>
 struct PolDist {
   float cdf[NO - 1];   // running sum of the probabilities (the draw's comparison values)
@@ -224,6 +229,7 @@ struct PolDist {
 
 template <int NO>
 __device__ __forceinline__ PolDist<NO> policy_dist(const float* src, const float* hb, int A, float* probs_row) {
+  if constexpr (pol_unpadded(NO)) A = NO - 1;
   PolDist<NO> d;
   float logit[NO];
 #pragma unroll
@@ -260,6 +266,7 @@ __device__ __forceinline__ float policy_uniform(uint32_t gid, uint32_t episode, 
 template <int NO>
 __device__ __forceinline__ int policy_pick(const float* cdf, const float* lp, int last_nz, int A, float u,
                                            float& log_prob) {
+  if constexpr (pol_unpadded(NO)) A = NO - 1;
   int act = 0;
 #pragma unroll
   for (int o = 0; o < NO - 1; ++o) act += (o < A && cdf[o] <= u) ? 1 : 0;
