@@ -78,6 +78,9 @@ def parse():
                    help="large-batch leg (2^20 envs/GPU, W=10: past the 256-MB Infinity Cache): timed steps "
                         "(0 = skip)")
     p.add_argument("--large-envs", type=int, default=1 << 20)
+    p.add_argument("--blocks-launches", type=int, default=200,
+                   help="prep_state2 block-count leg (SURVEY 8(f) rank 3, be_observe_blocks): timed launches "
+                        "at --envs and at --large-envs (0 = skip)")
     p.add_argument("--from-reset-steps", type=int, default=400,
                    help="the headline step timed straight from a fresh reset (no settle): timed steps (0 = skip)")
     return p.parse_args()
@@ -529,6 +532,49 @@ def from_reset_leg(args, gb, dev, rank, world, stream):
     return res
 
 
+def blocks_leg(args, gb, dev, rank, world, stream):
+    """prep_state2 block counts (be_observe_blocks) of every env of a batch
+    that has stepped (obstacles spread), u8 and f32 rows, graph-replayed launches; at --envs and at
+    --large-envs (DRAM-resident).  HBM-bound: agent + goal + every obstacle read (8 + 4 (Ns + Nd) B),
+    the 29-byte (u8) or 116-byte (f32) row written."""
+    import ctypes as C
+    import torch
+    res = {}
+    for N, T in ((args.envs, args.blocks_launches), (args.large_envs, max(1, args.blocks_launches // 4))):
+        cfg = gb.EnvConfig()
+        env = gb.BatchedBallEnv(N, 10, cfg, device=dev, seed=0xB10C5, env_offset=rank * N)
+        env.reset()
+        for _ in range(20):
+            env.step()
+        lib, ctx, st = env._lib, env._ctx, C.byref(env._st)
+        leg = {}
+        for kind, dt, rowb in (("u8", torch.uint8, 29), ("f32", torch.float32, 116)):
+            out = torch.empty(N, 29, dtype=dt, device=dev)
+            u8p, f32p = (out.data_ptr(), None) if kind == "u8" else (None, out.data_ptr())
+            g = torch.cuda.CUDAGraph()
+            cap = torch.cuda.Stream(dev)
+            with torch.cuda.graph(g, stream=cap):
+                sp = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+                for _ in range(T):
+                    lib.be_observe_blocks(ctx, st, C.c_void_p(u8p), C.c_void_p(f32p), sp)
+            g.replay()
+            el, ms = timed_graph_steps([g], T, dev, stream, world)
+            B = 8 + 4 * (cfg.num_static + cfg.num_dynamic) + rowb
+            ach = B * N / (ms * 1e-3) / 1e9
+            leg[kind] = {"value": T * N * world / el, "unit": "env-rows/s", "kernel_us_mean": ms * 1e3,
+                         "bytes_per_env": B,
+                         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": ach / HBM_PEAK_GBS}}
+            del g
+        env.status()
+        env.close()
+        res[f"envs_{N}"] = leg
+    res["workload"] = ("be_observe_blocks (prep_state2, examples/ball_env_reinforce.py:130-172): 29 block counts "
+                       "per env from the engine state, 13 static + 5 dynamic obstacles, graph-replayed launches")
+    res["kernel"] = "blocks_kernel"
+    return res
+
+
 def committed_pmc(fname, kernel_sub, units):
     """A committed tools/pmc_report.py profile, if it was taken on this kernel at this many units
     per dispatch (else None)."""
@@ -793,6 +839,7 @@ def main():
     pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
     board_res = board_leg(args, gb, dev, rank, world, stream) if args.board_steps > 0 else None
     roll_res = rollout_leg(args, gb, dev, rank, world, stream) if args.rollout_steps > 0 else None
+    blocks_res = blocks_leg(args, gb, dev, rank, world, stream) if args.blocks_launches > 0 else None
 
     if rank == 0:
         line = {
@@ -827,6 +874,7 @@ def main():
             "policy_rollout": pol_res,
             "board_profile": board_res,
             "fused_rollout": roll_res,
+            "blocks_obs": blocks_res,
         }
         print(json.dumps(line), flush=True)
     env.close()

@@ -9,8 +9,13 @@
 //
 // One lane per env (the env index is the coalesced axis of every state array); the 29
 // counters live in 8 packed 32-bit registers and each obstacle adds 1 << 8*(cell & 3) to
-// the word of its cell with selects (no scratch memory); rows are written as bytes.
-// All integer: the reference's sign(x)*(x-10)//20 on integer coordinates is exact.
+// the word of its cell with selects (no scratch memory).  All integer: the reference's
+// sign(x)*(x-10)//20 on integer coordinates is exact.
+//
+// HBM-bound (80 B of state read, 29 B / 116 B of rows written per env): each wave's 64 rows
+// are one contiguous run of the output (64 x 29 B = 116 16-B chunks; f32: 464), so the rows go
+// through a per-wave LDS stage and out in 16-B stores, instead of 29 byte (dword) stores per
+// lane at a 29-B (116-B) stride.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -31,17 +36,32 @@ struct BParams {
   int32_t n, ns, nd;
 };
 
+// a wave's n contiguous 16-B chunks from its LDS stage to dst (16-B aligned)
+__device__ __forceinline__ void copy_chunks(const uint8_t* stage, uint8_t* dst, int n, int lane) {
+  for (int c = lane; c < n; c += 64)
+    reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(stage)[c];
+}
+
+constexpr int BLK_ROW = 29, BLK_WAVE_U8 = 64 * BLK_ROW, BLK_WAVE_F32 = 64 * BLK_ROW * 4;
+
+// dynamic LDS: 4 wave stages of BLK_WAVE_U8 bytes, or BLK_WAVE_F32 when f32 rows are asked for (a
+// u8-only launch keeps 7.4 KB per block, so LDS does not cap the waves per CU)
 __global__ __launch_bounds__(256) void blocks_kernel(BParams p) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= p.n) return;
-  const int32_t a = p.agent[i], gl = p.goal[i];
+  extern __shared__ __align__(16) uint8_t smem[];
+  const int tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int i = blockIdx.x * 256 + tid, e0 = blockIdx.x * 256 + w * 64;
+  const int nrows = max(0, min(64, p.n - e0));            // this wave's rows (uniform)
+  if (nrows == 0) return;
+  const bool valid = i < p.n;
+  const int ic = valid ? i : p.n - 1;
+  const int32_t a = p.agent[ic], gl = p.goal[ic];
   const int ax = px(a), ay = py(a), dx = px(gl) - ax, dy = py(gl) - ay;
-  uint32_t w[8] = {0, 0, 0, 0, 1u, 0, 0, 0};     // byte 16 (the agent's cell) = 1
+  uint32_t w8[8] = {0, 0, 0, 0, 1u, 0, 0, 0};     // byte 16 (the agent's cell) = 1
   const int quad = dx >= 0 ? (dy >= 0 ? 1 : 2) : (dy >= 0 ? 0 : 3);
-  w[0] = 1u << (8 * quad);
+  w8[0] = 1u << (8 * quad);
   const int nobs = p.ns + p.nd;
   for (int k = 0; k < nobs; ++k) {
-    const int32_t o = k < p.ns ? p.static_obs[(int64_t)k * p.n + i] : p.dyn_obs[(int64_t)(k - p.ns) * p.n + i];
+    const int32_t o = k < p.ns ? p.static_obs[(int64_t)k * p.n + ic] : p.dyn_obs[(int64_t)(k - p.ns) * p.n + ic];
     const int xd = ax - px(o), yd = ay - py(o);
     int xb = 0, yb = 0;
     if (xd != 0 && yd != 0) {
@@ -52,15 +72,41 @@ __global__ __launch_bounds__(256) void blocks_kernel(BParams p) {
     const int cell = 16 + 5 * yb + xb;           // byte index 4 + (12 + 5 yb + xb)
     const uint32_t inc = in ? 1u << (8 * (cell & 3)) : 0u;
 #pragma unroll
-    for (int q = 1; q < 8; ++q) w[q] += (cell >> 2) == q ? inc : 0u;
+    for (int q = 1; q < 8; ++q) w8[q] += (cell >> 2) == q ? inc : 0u;
   }
-  uint8_t* row = p.out ? p.out + (int64_t)i * 29 : nullptr;
-  float* rowf = p.out_f32 ? p.out_f32 + (int64_t)i * 29 : nullptr;
+  uint8_t* stage = smem + w * (p.out_f32 ? BLK_WAVE_F32 : BLK_WAVE_U8);
+  const bool full = nrows == 64;
+  // wave barrier between a stage's writes and its copy-out (and the next format's writes)
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  if (p.out) {
+    uint8_t* row = stage + lane * BLK_ROW;
 #pragma unroll
-  for (int b = 0; b < 29; ++b) {
-    const uint8_t v = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-    if (row) row[b] = v;
-    if (rowf) rowf[b] = (float)v;
+    for (int b = 0; b < BLK_ROW; ++b) row[b] = (uint8_t)(w8[b >> 2] >> (8 * (b & 3)));
+    wave_sync();
+    uint8_t* dst = p.out + (int64_t)e0 * BLK_ROW;
+    if (full && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+      copy_chunks(stage, dst, BLK_WAVE_U8 / 16, lane);
+    } else {
+      for (int b = lane; b < nrows * BLK_ROW; b += 64) dst[b] = stage[b];
+    }
+    wave_sync();
+  }
+  if (p.out_f32) {
+    float* rowf = reinterpret_cast<float*>(stage) + lane * BLK_ROW;
+#pragma unroll
+    for (int b = 0; b < BLK_ROW; ++b) rowf[b] = (float)(uint8_t)(w8[b >> 2] >> (8 * (b & 3)));
+    wave_sync();
+    float* dst = p.out_f32 + (int64_t)e0 * BLK_ROW;
+    if (full && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+      copy_chunks(stage, reinterpret_cast<uint8_t*>(dst), BLK_WAVE_F32 / 16, lane);
+    } else {
+      const float* sf = reinterpret_cast<const float*>(stage);
+      for (int b = lane; b < nrows * BLK_ROW; b += 64) dst[b] = sf[b];
+    }
   }
 }
 
@@ -78,7 +124,8 @@ int be_observe_blocks(be_ctx* ctx, const be_state* st, uint8_t* out, float* out_
   if (e == hipSuccess && cur != cv.device) e = hipSetDevice(cv.device);
   if (e != hipSuccess) return be_ctx_fail(ctx, BE_E_HIP, hipGetErrorString(e));
   BParams p{st->agent, st->goal, st->static_obs, st->dyn_obs, out, out_f32, cv.num_envs, cv.num_static, cv.num_dynamic};
-  hipLaunchKernelGGL(blocks_kernel, dim3((unsigned)((cv.num_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p);
+  const size_t lds = 4 * (size_t)(out_f32 ? BLK_WAVE_F32 : BLK_WAVE_U8);
+  hipLaunchKernelGGL(blocks_kernel, dim3((unsigned)((cv.num_envs + 255) / 256)), dim3(256), lds, (hipStream_t)stream, p);
   e = hipGetLastError();
   if (e != hipSuccess) return be_ctx_fail(ctx, BE_E_HIP, hipGetErrorString(e));
   return BE_OK;

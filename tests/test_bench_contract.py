@@ -27,7 +27,7 @@ def test_cpu_baseline_leg_small_sample():
 def test_bench_json_line(gpu):
     cmd = [sys.executable, "bench.py", "--steps", "20", "--warmup", "5", "--settle", "60", "--no-cpu-baseline",
            "--policy-steps", "20", "--torch-policy-steps", "5", "--board-steps", "20", "--rollout-steps", "100",
-           "--config2-steps", "50", "--large-steps", "20", "--from-reset-steps", "20"]
+           "--config2-steps", "50", "--large-steps", "20", "--from-reset-steps", "20", "--blocks-launches", "8"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -46,11 +46,16 @@ def test_bench_json_line(gpu):
     assert d["config2"]["roofline"]["bytes_per_env_step"] == 315
     assert d["large_batch"]["envs_per_gpu"] == 1 << 20 and d["large_batch"]["steps"] == 20
     assert d["from_reset"]["untimed_steps_since_reset"] == 0
+    for n in (65536, 1 << 20):
+        for kind, rowb in (("u8", 29), ("f32", 116)):
+            leg = d["blocks_obs"][f"envs_{n}"][kind]
+            assert leg["value"] > 0 and leg["bytes_per_env"] == 8 + 4 * 18 + rowb and leg["roofline"]["frac"] > 0
     assert "cpu_baseline" not in d or d["cpu_baseline"] is None
 
 
 _ONLY_HEADLINE = ["--no-cpu-baseline", "--policy-steps", "0", "--board-steps", "0", "--rollout-steps", "0",
-                  "--cold-steps", "0", "--config2-steps", "0", "--large-steps", "0", "--from-reset-steps", "0"]
+                  "--cold-steps", "0", "--config2-steps", "0", "--large-steps", "0", "--from-reset-steps", "0",
+                  "--blocks-launches", "0"]
 
 
 def _bench_line(args, timeout=110):
@@ -103,7 +108,7 @@ def test_bench_rccl_one_rank(gpu):
            f"--master-port={port}", "bench.py", "--gpus", "1", "--dist-backend", "nccl", "--steps", "20", "--warmup", "5",
            "--settle", "60", "--rollout-steps", "100", "--policy-steps", "20", "--torch-policy-steps", "0",
            "--board-steps", "20", "--cold-steps", "0", "--config2-steps", "20", "--large-steps", "0",
-           "--from-reset-steps", "0", "--no-cpu-baseline"]
+           "--from-reset-steps", "0", "--blocks-launches", "0", "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110,
                        env=dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]

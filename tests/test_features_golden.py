@@ -77,5 +77,7 @@ def test_gpu_blocks_vs_oracle_rollout(gpu):
         if t % 5 == 0:
             st = {k: getattr(env, k).cpu().numpy().copy() for k in env.STATE_KEYS}
             st["episode"] = st["episode"].view(np.uint32)
-            np.testing.assert_array_equal(env.observe_blocks().cpu().numpy(), oracle.observe_blocks(cfg, st))
+            ref = oracle.observe_blocks(cfg, st)
+            np.testing.assert_array_equal(env.observe_blocks().cpu().numpy(), ref)
+            np.testing.assert_array_equal(env.observe_blocks(f32=True).cpu().numpy(), ref.astype(np.float32))
     env.close()

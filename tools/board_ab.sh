@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/board_ab
-ARGS="--no-cpu-baseline --steps 10 --warmup 2 --policy-steps 0 --rollout-steps 0 --board-steps 1000 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0"
+ARGS="--no-cpu-baseline --steps 10 --warmup 2 --policy-steps 0 --rollout-steps 0 --board-steps 1000 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0"
 for r in 1 2; do
   for v in new ${B:-boardold}; do
     if [ $v = new ]; then L=""; else L=tools/diag/$v/libballenv.so; fi

@@ -27,16 +27,16 @@ tail -c 400 $O/bench.log; echo
 if [ "${PROFILE:-1}" = "1" ]; then
   step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_head -o run -- \
       python bench.py --no-cpu-baseline --steps 300 --warmup 20 --policy-steps 0 --board-steps 0 --rollout-steps 0 \
-      --cold-steps 0 --config2-steps 1000 --large-steps 200 --from-reset-steps 0
+      --cold-steps 0 --config2-steps 1000 --large-steps 200 --from-reset-steps 0 --blocks-launches 0
   find $O/prof_head -name "*kernel_stats.csv" -exec head -6 {} \;
   step rocprof_fused 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_fused -o run -- \
       python bench.py --no-cpu-baseline --steps 10 --warmup 5 --policy-steps 200 --torch-policy-steps 0 --board-steps 200 \
-      --rollout-steps 1000 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0
+      --rollout-steps 1000 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0
   find $O/prof_fused -name "*kernel_stats.csv" -exec head -8 {} \;
 fi
 if [ "${PMC:-1}" = "1" ]; then
   step pmc_c2_large 600 bash tools/pmc_passes.sh r3c/pmc --no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 \
-      --board-steps 0 --rollout-steps 0 --cold-steps 0 --from-reset-steps 0 --config2-steps 200 --large-steps 100
+      --board-steps 0 --rollout-steps 0 --cold-steps 0 --from-reset-steps 0 --blocks-launches 0 --config2-steps 200 --large-steps 100
   python tools/pmc_report.py $O/pmc "stepw_kernel<5, 13, 5, 8>" 4096 --out $O/r03_pmc_config2.json > /dev/null
   python tools/pmc_report.py $O/pmc "be_kernel<10, 0, 13, 5>" 1048576 --out $O/r03_pmc_large_batch.json > /dev/null
   step pmc_step 700 bash tools/pmc_bench.sh
