@@ -153,25 +153,36 @@ __device__ void features(const BParams& p, float4* out, double ax, double ay, do
   float f[20];
 #pragma unroll
   for (int k = 0; k < 20; ++k) f[k] = 0.f;
-  // calcDistanceFromGoal (:132-144): floor(hypot / 5), capped at 5
-#ifdef BE_BOARD_DIAG_NOHYPOT   // diagnostics (timing placebo, wrong features)
-  const double dg = floor((fabs(ax - gx) + fabs(ay - gy)) / 5.0);
-#else
-  const double dg = floor(hypot(ax - gx, ay - gy) / 5.0);
-#endif
-  f[0] = (float)(dg > 5.0 ? 5.0 : dg);
-  // relativeGoalPos (:146-166): angle between (0, 1) and (gx - ax, gy - ay)
   const double vx = gx - ax, vy = gy - ay;
-  const double nv = sqrt(__dadd_rn(__dmul_rn(vx, vx), __dmul_rn(vy, vy)));
+  const double nv = sqrt(__dadd_rn(__dmul_rn(vx, vx), __dmul_rn(vy, vy)));   // |goal - agent|
+  // calcDistanceFromGoal (:132-144): floor(hypot(ax - gx, ay - gy) / 5), capped at 5.  nv is the
+  // same length (correctly rounded sqrt of the rounded sum; within a few ulps of hypot's 1-ulp
+  // result), so floor(nv / 5) is floor(hypot / 5) unless nv / 5 lies within 1e-9 of an integer:
+  // only a wave with such a lane (never seen in practice) evaluates hypot.
+  const double tq = nv / 5.0, tf = floor(tq);
+  double dg = tf;
+#ifndef BE_BOARD_ALWAYS_HYPOT   // (A/B builds)
+  if (tq - tf < 1e-9 || tf + 1.0 - tq < 1e-9)
+#endif
+    dg = floor(hypot(ax - gx, ay - gy) / 5.0);
+  f[0] = (float)(dg > 5.0 ? 5.0 : dg);
+  // relativeGoalPos (:146-166): angle between (0, 1) and (gx - ax, gy - ay), acos(c) of the
+  // clipped cosine c.  acos decreases, so ang < pi/4 is c > cos(pi/4) and ang > 3 pi/4 is
+  // c < -cos(pi/4); acos (1 ulp) only decides a lane within 1e-9 of those cuts.
   double c = nv > 0.0 ? vy / nv : 0.0;
   c = c < -1.0 ? -1.0 : (c > 1.0 ? 1.0 : c);
-#ifdef BE_BOARD_DIAG_NOACOS    // diagnostics (timing placebo, wrong features)
-  const double ang = 1.5 - c;
-#else
-  const double ang = acos(c);
+  constexpr double COS_PI4 = 0.70710678118654752;
+  int bin;   // 0: ang < pi/4, 1: pi/4 < ang < 3 pi/4, 2: otherwise
+  bin = c > COS_PI4 ? 0 : (c > -COS_PI4 ? 1 : 2);
+#ifndef BE_BOARD_ALWAYS_ACOS    // (A/B builds)
+  if (fabs(fabs(c) - COS_PI4) < 1e-9)
 #endif
-  if (ang < PI / 4) f[1] = 1.f;
-  else if (ang > PI / 4 && ang < PI * 3 / 4) { if (vx > 0) f[2] = 1.f; else f[4] = 1.f; }
+  {
+    const double ang = acos(c);
+    bin = ang < PI / 4 ? 0 : ((ang > PI / 4 && ang < PI * 3 / 4) ? 1 : 2);
+  }
+  if (bin == 0) f[1] = 1.f;
+  else if (bin == 1) { if (vx > 0) f[2] = 1.f; else f[4] = 1.f; }
   else f[3] = 1.f;
   // density (:91-112), speed/orientation (:115-130), social forces (:170-193)
   // branch-free over this lane's slots (slots past ns are masked out), so the obstacles' f64
@@ -414,6 +425,74 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
   }
 }
 
+// Single-chain reset pass (1 <= ns <= 12), one finished env at a time on all 64 lanes: lane 0
+// draws the goal, lanes 1..FA agent attempts 0..FA-1 and lane FS + a*ns + k attempt a of static
+// k (a < (64 - FS) / ns), each lane with its own counter of the layout above -- one Philox chain
+// per lane where the general passes run three (goal, agent attempts, static attempts) one after
+// the other.  The agent is checked against the goal (lane 0's draw, read back), then the statics
+// against both; each rejection loop takes its first accepted attempt in attempt order, as the
+// general passes do, so an env whose loops all accept within these attempts gets the same state
+// bit for bit.  The others (the agent rejected FA times, or a static rejected every time) are
+// returned in the mask and take the general passes.
+constexpr int FAST_AG = 12, FAST_S0 = FAST_AG + 1;
+template <int MAXS>
+__device__ unsigned long long wave_board_resets_fast(const BParams& p, unsigned long long m, uint32_t gid,
+                                                     uint32_t episode_new, double& ax, double& ay, double& gx,
+                                                     double& gy, double& d0, double& total, int32_t (&so)[MAXS]) {
+  const int lane = (int)(threadIdx.x & 63), ns = p.ns;
+  const int per = (64 - FAST_S0) / ns;
+  const int sl = lane - FAST_S0, k_l = sl >= 0 ? sl % ns : 0, a_l = sl >= 0 ? sl / ns : 0;
+  const bool is_ag = lane >= 1 && lane <= FAST_AG, is_st = sl >= 0 && a_l < per;
+  const uint32_t sub = is_ag ? (1u << 20) | (uint32_t)(lane - 1)
+                             : (is_st ? (2u << 20) | ((uint32_t)k_l << 12) | (uint32_t)a_l : 0u);
+  unsigned long long kbase = 0;                                 // lanes (a, k = 0)
+  for (int a = 0; a < per; ++a) kbase |= 1ull << (FAST_S0 + a * ns);
+  unsigned long long rest = 0;
+  while (m) {
+    const int l = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)gid, l);
+    const uint32_t ep = (uint32_t)__builtin_amdgcn_readlane((int)episode_new, l);
+    const u4 b = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, sub), p.seed);
+    const double r0 = ranf2(b.x, b.y), r1 = ranf2(b.z, b.w);
+    // goal (ballenv_pygame.py:462-463): lane 0's block
+    const double rgx = readlane_f64((double)(p.W - p.sgx) + r0 * (double)p.sgx, 0);
+    const double rgy = readlane_f64((double)(p.H - p.sgy) + r1 * (double)p.sgy, 0);
+    // candidates: agent attempts (ranf) or static attempts (randint)
+    const int ox = p.sox + (int)__umulhi(b.x, (uint32_t)(p.W - 2 * p.sox));
+    const int oy = p.soy + (int)__umulhi(b.y, (uint32_t)(p.H - 2 * p.soy));
+    const double fx = is_ag ? r0 * (double)p.sax : (double)ox, fy = is_ag ? r1 * (double)p.say : (double)oy;
+    const double dg = dist2(fx, fy, rgx, rgy);                  // |candidate - goal| (symmetric in sign)
+    // agent (:464-481): the first attempt with dist >= min_spawn; state[2] = attempt 0's distance
+    const unsigned long long oka = __ballot(is_ag && !(dg < p.min_spawn));
+    if (!oka) { rest |= 1ull << l; continue; }
+    const double d0v = readlane_f64(dg, 1);
+    const int qa = __ffsll((long long)oka) - 1;
+    const double rax = readlane_f64(fx, qa), ray = readlane_f64(fy, qa);
+    // statics (:489-498): not within thresh of the agent or the goal
+    const bool oks = is_st && dist2(fx, fy, rax, ray) - p.thr_agent > p.r_collide && dg - p.thr_goal > p.r_collide;
+    const unsigned long long okm = __ballot(oks);
+    const int32_t cand = (int32_t)(((uint32_t)ox & 0xFFFFu) | ((uint32_t)oy << 16));
+    int32_t got[MAXS];
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k) {
+      got[k] = 0;
+      if (k >= ns) continue;
+      const unsigned long long hit = okm & (kbase << k);
+      if (!hit) { all = false; continue; }
+      got[k] = __builtin_amdgcn_readlane(cand, __ffsll((long long)hit) - 1);
+    }
+    if (!all) { rest |= 1ull << l; continue; }
+    if (lane == l) {
+      gx = rgx; gy = rgy; ax = rax; ay = ray; d0 = d0v; total = dist2(rax, ray, rgx, rgy);   // total_distance
+#pragma unroll
+      for (int k = 0; k < MAXS; ++k) so[k] = got[k];
+    }
+  }
+  return rest;
+}
+
 // MAXS: compile-time bound on the static-obstacle count (4 .. 32), so the obstacle loops unroll
 // with a runtime guard and the positions stay in registers (no scratch).  L lanes per env (1 or
 // 2): every lane holds the env's whole state; lane h runs the collision test and the feature
@@ -537,16 +616,24 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     if (p.tape) {   // parity mode: the reference's draw order, on the env's own lane(s)
       if (do_reset) reset_env(p, i, episode + 1u, ax, ay, gx, gy, dist, total, so);
     } else {
-      const unsigned long long m = __ballot(do_reset && h == 0);
-      if (m) {   // several finished envs: 2 or 4 per pass (ns must fit a slot: ns <= 64 / P)
-        const int nf = __popcll(m);
+      const unsigned long long m0 = __ballot(do_reset && h == 0);
+      if (m0) {
         const uint32_t g = (uint32_t)p.gid0 + (uint32_t)i;
-        if constexpr (MAXS > 16) {   // (ns > 16 never fits two slots)
-          wave_board_resets<MAXS, 1>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
-        } else {
-          if (nf == 1) wave_board_resets<MAXS, 1>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
-          else if (nf == 2 || p.ns > 8) wave_board_resets<MAXS, 2>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
-          else wave_board_resets<MAXS, 4>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+        unsigned long long m = m0;
+#ifndef BE_BOARD_NO_FAST_RESET   // (A/B builds: the general passes only)
+        if constexpr (MAXS <= 12) {   // one Philox chain per reset; the rare rest take the general passes
+          if (p.ns >= 1) m = wave_board_resets_fast<MAXS>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+        }
+#endif
+        if (m) {   // several finished envs: 2 or 4 per pass (ns must fit a slot: ns <= 64 / P)
+          const int nf = __popcll(m);
+          if constexpr (MAXS > 16) {   // (ns > 16 never fits two slots)
+            wave_board_resets<MAXS, 1>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+          } else {
+            if (nf == 1) wave_board_resets<MAXS, 1>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+            else if (nf == 2 || p.ns > 8) wave_board_resets<MAXS, 2>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+            else wave_board_resets<MAXS, 4>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
+          }
         }
         if constexpr (L == 2) {   // the owner (lane 0) took the new state: its partner copies it
           if (__ballot(do_reset)) {

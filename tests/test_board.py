@@ -184,14 +184,18 @@ def test_gpu_board_rollout_matches_steps(gpu, use_deltas):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ns", [6, 8, 0])
-def test_gpu_board_philox_resets_vs_oracle(gpu, ns):
+@pytest.mark.parametrize("ns,over", [(6, {}), (8, {}), (0, {}), (12, {}), (6, {"min_spawn_dist": 65.0}),
+                                     (8, {"spawn_thresh_agent": 30.0, "spawn_thresh_goal": 25.0})])
+def test_gpu_board_philox_resets_vs_oracle(gpu, ns, over):
     """Philox-mode resets (be_board_reset without a tape, and the autoreset inside be_board_step)
     bit-exact against the oracle's sequential restatement of the engine's draw layout
     (orc_board_reset_philox): a full reset, a masked reset, then 40 random moves with autoreset.
-    The draws are the engine's own (Philox), so this pins the layout, not the reference."""
+    The draws are the engine's own (Philox), so this pins the layout, not the reference.
+    The single-chain pass (1 <= ns <= 12) hands envs whose rejection loops need more attempts
+    than it draws to the general passes: ns = 12 (four attempts per static), a min_spawn of 65
+    (the agent rejected 12 times in a row for ~9 % of resets) and wide static thresholds make those common."""
     N, seed, off = 5000, 0x5EED, 12345
-    b = make_board(gpu, N, ns, seed=seed, env_offset=off, autoreset=True)
+    b = make_board(gpu, N, ns, seed=seed, env_offset=off, autoreset=True, **over)
     cfg = b.cfg
     st = oracle.board_new_state(cfg)
     rng = np.random.default_rng(ns)
