@@ -1997,18 +1997,29 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const int32_t agent0 = ld_s(p.agent, ic), goal0 = ld_s(p.goal, ic);
   int32_t dp[SD], so[SS];
   int dgi[SD];
+  // (the slot offsets k * N are kept apart from + ic: fused into one v_mad_u64_u32, whose 64-bit
+  // addend pair took a pending load's register as its high half, the compiler waited for the first
+  // loads before issuing these -- a second memory latency in the prologue)
 #pragma unroll
   for (int j = 0; j < SD; ++j) {
-    const uint32_t e = (uint32_t)min(L * j + h, NDC - 1) * (uint32_t)N + ic;
+    uint32_t kn = (uint32_t)min(L * j + h, NDC - 1) * (uint32_t)N;
+    asm volatile("" : "+v"(kn));
+    const uint32_t e = kn + ic;
     dp[j] = ld_s(p.dyn_obs, e);
     dgi[j] = ld_s(p.dyn_goal, e);
   }
 #pragma unroll
-  for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
-  const double old_dist = p.prev_read ? ld_s(p.prev_dist, ic) : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
+  for (int j = 0; j < SS; ++j) {
+    uint32_t kn = (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N;
+    asm volatile("" : "+v"(kn));
+    so[j] = ld_s(p.static_obs, kn + ic);
+  }
+  const double old_read = ld_s(p.prev_dist, ic);   // (read even when unused: no branch among the loads)
   const double total = ld_s(p.total_dist, ic);
   double ret = ld_s(p.ep_return, ic);
   const int a = ld_s(p.actions, ic);
+  __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any of them is used
+  const double old_dist = p.prev_read ? old_read : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
   double* const slot = p.stats ? p.stats + (size_t)blockIdx.x * 8 : nullptr;
   double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sp2 = sp0;
   if (slot && tid == 0) {   // the block's stats slot, read now (wave 0 folds into it)
@@ -2593,10 +2604,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
   if constexpr (POL) {
     // the packed policy image, once per launch; the current obs rows (obs of the state)
     const uint4* src = reinterpret_cast<const uint4*>(p.pol_img);
-    for (int k = tid; k < p.pol_bytes / 16; k += BLOCK_THREADS) reinterpret_cast<uint4*>(pimg)[k] = src[k];
+    stage_image<BLOCK_THREADS, 8>(reinterpret_cast<uint4*>(pimg), src, p.pol_bytes / 16, tid);
     const int bytes = nrows * F;
     const uint8_t* orow = p.obs_in + (size_t)e0 * F;
-    for (int v = lane; v < bytes / 16; v += 64) reinterpret_cast<uint4*>(stage)[v] = reinterpret_cast<const uint4*>(orow)[v];
+    stage_image<64, 8>(reinterpret_cast<uint4*>(stage), reinterpret_cast<const uint4*>(orow), bytes / 16, lane);
     for (int b = (bytes & ~15) + lane; b < bytes; b += 64) stage[b] = orow[b];
     if (tid < 3) reinterpret_cast<int*>(pimg + PL.count)[tid] = 0;
   }

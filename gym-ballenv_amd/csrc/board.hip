@@ -32,8 +32,9 @@
 // One lane per env; the env index is the unit-stride HBM axis of every array.  Resets
 // (reset(), or autoreset inside step) draw from a tape on the env's own lane (parity mode:
 // the reference's ranf/randint values in call order), or from Philox(seed; gid, episode, 0,
-// BOARD<<24 | sub), wave-cooperatively (wave_board_resets: every rejection loop becomes one
-// ballot over 64 candidate attempts).
+// BOARD<<24 | sub), wave-cooperatively (wave_board_resets_fast: one Philox chain per lane covers
+// the goal and the first attempts of every rejection loop; wave_board_resets, for the rare env
+// that needs more: every rejection loop becomes one ballot over 64 candidate attempts).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -57,6 +58,7 @@ constexpr int BDIAG_WAVES = 1 << 14;
 __device__ unsigned long long g_bdiag[BDIAG_WAVES][8];
 #define BPH_INIT unsigned long long bph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bph_t = __builtin_amdgcn_s_memtime()
 #define BPH(k) do { const unsigned long long bph_n = __builtin_amdgcn_s_memtime(); bph_acc[k] += bph_n - bph_t; bph_t = bph_n; } while (0)
+#define BCOUNT(k, v) (bph_acc[k] += (unsigned long long)(v))   // counts (not cycles) in slots 5..7
 #define BPH_STORE do { \
     const int bph_w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64); \
     if ((threadIdx.x & 63) == 0 && bph_w < BDIAG_WAVES) \
@@ -65,6 +67,7 @@ __device__ unsigned long long g_bdiag[BDIAG_WAVES][8];
 #else
 #define BPH_INIT ((void)0)
 #define BPH(k) ((void)0)
+#define BCOUNT(k, v) ((void)0)
 #define BPH_STORE ((void)0)
 #endif
 constexpr int BOARD_REJECT_LIMIT = 4096;
@@ -92,6 +95,21 @@ struct BParams {
 __device__ __forceinline__ double dist2(double x1, double y1, double x2, double y2) {
   const double dx = x1 - x2, dy = y1 - y2;
   return sqrt(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)));   // math.sqrt(math.pow(dx,2)+math.pow(dy,2))
+}
+// Per-step outputs and state of be_board_step: write-through stores (sc1, a relaxed agent-scope
+// atomic store; the features as sc1 buffer stores), so they drain while the wave runs instead of in
+// the kernel-end L2 write-back -- as the step kernels of ballenv.hip do: 8.75 -> 8.22 us per step at
+// 65 536 envs; the fused rollout too (3.68 -> 3.62 us per step; profiles/r03_board_wt_ab.txt).
+#ifndef BE_BOARD_WT
+#define BE_BOARD_WT 1
+#endif
+#ifndef BE_BOARD_WT_ROLL
+#define BE_BOARD_WT_ROLL 1
+#endif
+template <bool WT, class T>
+__device__ __forceinline__ void bst(T* p, T v) {
+  if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
 }
 __device__ __forceinline__ int sx(int32_t p) { return (int)(int16_t)(p & 0xFFFF); }
 __device__ __forceinline__ int sy(int32_t p) { return p >> 16; }
@@ -502,20 +520,38 @@ __device__ unsigned long long wave_board_resets_fast(const BParams& p, unsigned 
 // A wave's feature rows (EPW x 80 B, contiguous in the output) from its LDS stage to HBM with
 // 16-byte stores in lane order: whole cache lines per store instruction, where a lane's own row
 // would scatter 5 stores over 64 rows at an 80-B stride.
-template <int EPW>
+template <int EPW, bool WT>
 __device__ __forceinline__ void copy_feat(const float4* stage, float* dst, int nrows, int lane) {
   const int nv = nrows * 5;
-  float4* d4 = reinterpret_cast<float4*>(dst);
+  if constexpr (WT) {   // nrows / dst are wave-uniform: a scalar descriptor whose size drops the tail
+    typedef int v4i_ __attribute__((ext_vector_type(4)));
+    const int nvu = __builtin_amdgcn_readfirstlane(nv);
+    const uint64_t du = (uint64_t)dst;
+    float* dstu = reinterpret_cast<float*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(du >> 32)) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)du));
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dstu, (short)0, nvu * 16, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < (EPW * 5 + 63) / 64; ++j) {
-    const int v = lane + 64 * j;
-    if (v < nv) d4[v] = stage[v];
+    for (int j = 0; j < (EPW * 5 + 63) / 64; ++j) {
+      const int v = lane + 64 * j;
+      const float4 x = stage[min(v, EPW * 5 - 1)];
+      const v4i_ y = {__builtin_bit_cast(int, x.x), __builtin_bit_cast(int, x.y), __builtin_bit_cast(int, x.z),
+                      __builtin_bit_cast(int, x.w)};
+      __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v * 16, 0, 16);   // aux 16 = sc1
+    }
+  } else {
+    float4* d4 = reinterpret_cast<float4*>(dst);
+#pragma unroll
+    for (int j = 0; j < (EPW * 5 + 63) / 64; ++j) {
+      const int v = lane + 64 * j;
+      if (v < nv) d4[v] = stage[v];
+    }
   }
 }
 
 template <int MAXS, bool ROLL, int L>
 __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   constexpr int SPL = (MAXS + L - 1) / L, EPW = 64 / L;
+  constexpr bool WT = ROLL ? (BE_BOARD_WT_ROLL != 0) : (BE_BOARD_WT != 0);
   __shared__ float4 s_feat[4][EPW * 5];   // per wave: its envs' feature rows
   const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
   float4* fstage = &s_feat[w][0];
@@ -526,7 +562,7 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    copy_feat<EPW>(fstage, p.features + row0 * 20, nrows, lane);
+    copy_feat<EPW, WT>(fstage, p.features + row0 * 20, nrows, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the next step's stage writes follow
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -606,9 +642,9 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       const bool trunc = !done && p.time_limit > 0 && len >= p.time_limit;
       done = done || trunc;
       if (valid) {   // the pair splits the per-step stores
-        if (h == 0) p.reward[row] = r;
-        if (h == L - 1) p.done[row] = done ? 1 : 0;
-        if (h == L - 1 && p.truncated) p.truncated[row] = trunc ? 1 : 0;
+        if (h == 0) bst<WT>(p.reward + row, r);
+        if (h == L - 1) bst<WT>(p.done + row, (uint8_t)(done ? 1 : 0));
+        if (h == L - 1 && p.truncated) bst<WT>(p.truncated + row, (uint8_t)(trunc ? 1 : 0));
       }
       do_reset = valid && done && p.autoreset;
       BPH(1);
@@ -625,6 +661,8 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
           if (p.ns >= 1) m = wave_board_resets_fast<MAXS>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
         }
 #endif
+        BCOUNT(5, __popcll(m0));
+        BCOUNT(6, __popcll(m));
         if (m) {   // several finished envs: 2 or 4 per pass (ns must fit a slot: ns <= 64 / P)
           const int nf = __popcll(m);
           if constexpr (MAXS > 16) {   // (ns > 16 never fits two slots)
@@ -668,18 +706,20 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   if (was_reset && h == L - 1) {
 #pragma unroll
     for (int k = 0; k < MAXS; ++k)
-      if (k < p.ns) p.statics[(int64_t)k * p.n + i] = so[k];
-    reinterpret_cast<double2*>(p.goal)[i] = make_double2(gx, gy);
-    p.total[i] = total;
-    p.episode[i] = episode;
+      if (k < p.ns) bst<WT>(p.statics + (int64_t)k * p.n + i, so[k]);
+    bst<WT>(p.goal + 2 * (int64_t)i, gx);
+    bst<WT>(p.goal + 2 * (int64_t)i + 1, gy);
+    bst<WT>(p.total + i, total);
+    bst<WT>(p.episode + i, episode);
   }
   if (h == 0) {
-    reinterpret_cast<double2*>(p.agent)[i] = make_double2(ax, ay);
-    p.dist[i] = dist;
+    bst<WT>(p.agent + 2 * (int64_t)i, ax);
+    bst<WT>(p.agent + 2 * (int64_t)i + 1, ay);
+    bst<WT>(p.dist + i, dist);
   }
   if (h == L - 1) {
-    p.ep_return[i] = ret;
-    p.ep_len[i] = len;
+    bst<WT>(p.ep_return + i, ret);
+    bst<WT>(p.ep_len + i, len);
   }
 }
 

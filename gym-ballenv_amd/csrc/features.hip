@@ -36,10 +36,26 @@ struct BParams {
   int32_t n, ns, nd;
 };
 
-// a wave's n contiguous 16-B chunks from its LDS stage to dst (16-B aligned)
-__device__ __forceinline__ void copy_chunks(const uint8_t* stage, uint8_t* dst, int n, int lane) {
-  for (int c = lane; c < n; c += 64)
-    reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(stage)[c];
+// a wave's N contiguous 16-B chunks from its LDS stage to dst (16-B aligned, wave-uniform) in one
+// unrolled pass: every LDS read issued before the first store, write-through (sc1) buffer stores --
+// they drain while the wave runs instead of in the kernel-end L2 write-back -- and a descriptor of
+// N * 16 bytes that drops the last pass's extra lanes (no branch)
+#ifndef BE_BLOCKS_AUX
+#define BE_BLOCKS_AUX 16   // cache-policy bits of the copy-out (gfx950: sc1 16; A/B builds: 0 plain)
+#endif
+template <int N>
+__device__ __forceinline__ void copy_chunks(const uint8_t* stage, uint8_t* dst, int lane) {
+  constexpr int IT = (N + 63) / 64;
+  typedef int v4i_ __attribute__((ext_vector_type(4)));
+  v4i_ x[IT];
+#pragma unroll
+  for (int j = 0; j < IT; ++j) x[j] = reinterpret_cast<const v4i_*>(stage)[min(lane + 64 * j, N - 1)];
+  const uint64_t du = (uint64_t)dst;
+  uint8_t* dstu = reinterpret_cast<uint8_t*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(du >> 32)) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)du));
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dstu, (short)0, N * 16, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < IT; ++j) __builtin_amdgcn_raw_buffer_store_b128(x[j], rsrc, (lane + 64 * j) * 16, 0, BE_BLOCKS_AUX);
 }
 
 constexpr int BLK_ROW = 29, BLK_WAVE_U8 = 64 * BLK_ROW, BLK_WAVE_F32 = 64 * BLK_ROW * 4;
@@ -59,20 +75,34 @@ __global__ __launch_bounds__(256) void blocks_kernel(BParams p) {
   uint32_t w8[8] = {0, 0, 0, 0, 1u, 0, 0, 0};     // byte 16 (the agent's cell) = 1
   const int quad = dx >= 0 ? (dy >= 0 ? 1 : 2) : (dy >= 0 ? 0 : 3);
   w8[0] = 1u << (8 * quad);
+  // obstacles in chunks of CH (the reference's 13 + 5 are one chunk): every load of a chunk is issued
+  // before the first is used (clamped to a real obstacle, the extra slots masked), so a wave waits
+  // for memory once per chunk instead of once per obstacle
+#ifndef BE_BLOCKS_CH
+#define BE_BLOCKS_CH 18   // obstacles per load chunk (A/B builds)
+#endif
+  constexpr int CH = BE_BLOCKS_CH;
   const int nobs = p.ns + p.nd;
-  for (int k = 0; k < nobs; ++k) {
-    const int32_t o = k < p.ns ? p.static_obs[(int64_t)k * p.n + ic] : p.dyn_obs[(int64_t)(k - p.ns) * p.n + ic];
-    const int xd = ax - px(o), yd = ay - py(o);
-    int xb = 0, yb = 0;
-    if (xd != 0 && yd != 0) {
-      xb = floordiv20(xd > 0 ? xd - 10 : 10 - xd);
-      yb = floordiv20(yd > 0 ? yd - 10 : 10 - yd);
-    }
-    const bool in = xb > -3 && xb < 3 && yb > -3 && yb < 3;
-    const int cell = 16 + 5 * yb + xb;           // byte index 4 + (12 + 5 yb + xb)
-    const uint32_t inc = in ? 1u << (8 * (cell & 3)) : 0u;
+  for (int k0 = 0; k0 < nobs; k0 += CH) {
+    int32_t o[CH];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) w8[q] += (cell >> 2) == q ? inc : 0u;
+    for (int j = 0; j < CH; ++j) {
+      const int k = min(k0 + j, nobs - 1);
+      const int32_t* src = k < p.ns ? p.static_obs + (int64_t)k * p.n : p.dyn_obs + (int64_t)(k - p.ns) * p.n;
+      o[j] = src[ic];
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int xd = ax - px(o[j]), yd = ay - py(o[j]);
+      const bool off = xd == 0 || yd == 0;   // the reference's sign(0) = 0: block 0 on both axes
+      const int xb = off ? 0 : floordiv20(xd > 0 ? xd - 10 : 10 - xd);
+      const int yb = off ? 0 : floordiv20(yd > 0 ? yd - 10 : 10 - yd);
+      const bool in = k0 + j < nobs && xb > -3 && xb < 3 && yb > -3 && yb < 3;
+      const int cell = 16 + 5 * yb + xb;         // byte index 4 + (12 + 5 yb + xb)
+      const uint32_t inc = in ? 1u << (8 * (cell & 3)) : 0u;
+#pragma unroll
+      for (int q = 1; q < 8; ++q) w8[q] += (cell >> 2) == q ? inc : 0u;
+    }
   }
   uint8_t* stage = smem + w * (p.out_f32 ? BLK_WAVE_F32 : BLK_WAVE_U8);
   const bool full = nrows == 64;
@@ -89,7 +119,7 @@ __global__ __launch_bounds__(256) void blocks_kernel(BParams p) {
     wave_sync();
     uint8_t* dst = p.out + (int64_t)e0 * BLK_ROW;
     if (full && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
-      copy_chunks(stage, dst, BLK_WAVE_U8 / 16, lane);
+      copy_chunks<BLK_WAVE_U8 / 16>(stage, dst, lane);
     } else {
       for (int b = lane; b < nrows * BLK_ROW; b += 64) dst[b] = stage[b];
     }
@@ -102,7 +132,7 @@ __global__ __launch_bounds__(256) void blocks_kernel(BParams p) {
     wave_sync();
     float* dst = p.out_f32 + (int64_t)e0 * BLK_ROW;
     if (full && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
-      copy_chunks(stage, reinterpret_cast<uint8_t*>(dst), BLK_WAVE_F32 / 16, lane);
+      copy_chunks<BLK_WAVE_F32 / 16>(stage, reinterpret_cast<uint8_t*>(dst), lane);
     } else {
       const float* sf = reinterpret_cast<const float*>(stage);
       for (int b = lane; b < nrows * BLK_ROW; b += 64) dst[b] = sf[b];

@@ -184,7 +184,7 @@ __global__ __launch_bounds__(POL_THREADS) void policy_kernel(PParams p) {
   if (!(p.dbg & 1)) {  // stage the packed weights (overlaps the scan's loads)
     const uint4* src = (const uint4*)p.img;
     const int n16 = p.img_bytes >> 4;
-    for (int i = tid; i < n16; i += POL_THREADS) pol_lds[i] = src[i];
+    stage_image<POL_THREADS, 6>(pol_lds, src, n16, tid);
   }
   if (g == 0 && tile0 + lane < p.n) {
     // obs bytes 0..3 must be exactly a quadrant one-hot for the table (any other input is dense)

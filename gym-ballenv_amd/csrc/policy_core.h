@@ -68,6 +68,22 @@ __device__ __forceinline__ void sum_outputs(const float (&part)[NO], float (&out
 
 
 // OR of x over lanes l, l^16, l^32, l^48
+// The packed image (global, 16-B words) into LDS by NT threads, U loads in flight per thread: a
+// plain `for (k = tid; k < n16; k += NT) dst[k] = src[k]` waits for each load before the next
+// one is issued (the LDS write needs it), one memory latency per pass -- 22 passes for the 89-KB
+// W=10 image in a 256-thread block.  Slots past the end re-read and re-write the last word (the same
+// value): no branch, which would let the compiler sink each load next to its write again.
+template <int NT, int U>
+__device__ __forceinline__ void stage_image(uint4* dst, const uint4* src, int n16, int tid) {
+  for (int k0 = tid; k0 < n16; k0 += U * NT) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[min(k0 + u * NT, n16 - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) dst[min(k0 + u * NT, n16 - 1)] = v[u];
+  }
+}
+
 __device__ __forceinline__ uint32_t or_groups(uint32_t x) {
   const auto a = __builtin_amdgcn_permlane16_swap(x, x, false, false);
   x = a[0] | a[1];

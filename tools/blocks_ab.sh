@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest tests/test_features_golden.py tests/test_b
 rc=$?; tail -2 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
 ARGS="--no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 --torch-policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 200"
 for r in 1 2; do
-  for v in new ${B:-old}; do
+  for v in new ${B:-old}; do   # B: one or more A/B builds
     if [ $v = new ]; then L=""; else L=tools/diag/$v/libballenv.so; fi
     BALLENV_LIB=$L timeout -k 10 200 python3 bench.py $ARGS > $O/$v.$r.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { echo "$v rc=$rc"; tail -5 $O/$v.$r.log; exit $rc; }

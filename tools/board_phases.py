@@ -31,4 +31,10 @@ for name, fn in (("be_board_step (last of 100 launches)", lambda: [b.step(acts[t
     print(f"{name}: cycles per wave-step p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max():.0f}")
     for k in range(5):
         print(f"  phase {k}: p50 {np.median(ph[:, k]):7.0f}  p90 {np.percentile(ph[:, k], 90):7.0f}  max {ph[:, k].max():7.0f}")
+    if steps == 1:   # slots 5 / 6: the wave's finished envs / those left to the general passes
+        nf, fb = cy[:N // 64, 5].astype(int), cy[:N // 64, 6].astype(int)
+        for v in sorted(set(nf.tolist())):
+            w = nf == v
+            print(f"  waves with {v} resets: {w.sum():4d}, phase 2 p50 {np.median(ph[w, 2]):6.0f} max {ph[w, 2].max():6.0f},"
+                  f" total p50 {np.median(tot[w]):6.0f} max {tot[w].max():6.0f}, general-pass envs {fb[w].sum()}")
 b.close()
