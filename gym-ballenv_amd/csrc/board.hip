@@ -602,18 +602,32 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   // mode 3 (be_board_rollout): p.steps steps with the state in registers, per-step outputs in
   // (steps, N, ...) rows; modes 0 / 1 are one pass of the same body
   const int steps = ROLL ? p.steps : 1;   // ROLL: the mode-3 instantiation
+  // the action table in LDS (a table read from memory is a second load on the move's chain), and
+  // the next step's action read one step ahead in the fused rollout, so its latency overlaps a step
+  __shared__ double s_act[2 * BE_BOARD_MAX_ACTIONS];
+  if (p.mode != 1 && p.actions) {   // (uniform)
+    if (threadIdx.x < 2 * p.num_actions) s_act[threadIdx.x] = (&p.tables->actions[0][0])[threadIdx.x];
+    __syncthreads();
+  }
+  int a_pf = 0;
+  double dx_pf = 0.0, dy_pf = 0.0;
+  auto fetch = [&](int s) {
+    const int64_t r = (int64_t)s * p.n + i;
+    if (p.actions) a_pf = p.actions[r];
+    else { dx_pf = p.deltas[2 * r]; dy_pf = p.deltas[2 * r + 1]; }
+  };
+  if (p.mode != 1) fetch(0);
   for (int s = 0; s < steps; ++s) {
     const int64_t row = (int64_t)s * p.n + i;   // this step's output row (i for modes 0 / 1)
     bool do_reset = valid && p.mode == 1 && (!p.mask || p.mask[i]);
     bool moved = false;
     if (p.mode != 1) {
-      double dx = 0.0, dy = 0.0;
+      double dx = dx_pf, dy = dy_pf;
+      int a = a_pf;
+      if (ROLL && s + 1 < steps) fetch(s + 1);
       if (p.actions) {
-        int a = p.actions[row];
         if (a >= p.num_actions) { atomicOr(p.status, BE_STATUS_BAD_ACTION); a = 0; }
-        dx = p.tables->actions[a][0]; dy = p.tables->actions[a][1];
-      } else {
-        dx = p.deltas[2 * row]; dy = p.deltas[2 * row + 1];
+        dx = s_act[2 * a]; dy = s_act[2 * a + 1];
       }
       BPH(0);
       // self.old_dist (:652) = |agent - goal|, which the previous step of this launch left in dist

@@ -75,11 +75,11 @@ __global__ __launch_bounds__(256) void blocks_kernel(BParams p) {
   uint32_t w8[8] = {0, 0, 0, 0, 1u, 0, 0, 0};     // byte 16 (the agent's cell) = 1
   const int quad = dx >= 0 ? (dy >= 0 ? 1 : 2) : (dy >= 0 ? 0 : 3);
   w8[0] = 1u << (8 * quad);
-  // obstacles in chunks of CH (the reference's 13 + 5 are one chunk): every load of a chunk is issued
-  // before the first is used (clamped to a real obstacle, the extra slots masked), so a wave waits
-  // for memory once per chunk instead of once per obstacle
+  // obstacles in chunks of CH: every load of a chunk is issued before the first is used (clamped to
+  // a real obstacle, the extra slots masked), so a wave waits for memory once per chunk instead of
+  // once per pair of obstacles
 #ifndef BE_BLOCKS_CH
-#define BE_BLOCKS_CH 18   // obstacles per load chunk (A/B builds)
+#define BE_BLOCKS_CH 6    // obstacles per load chunk (18: slower at 65 536 envs, profiles/r03_blocks_ab.txt)
 #endif
   constexpr int CH = BE_BLOCKS_CH;
   const int nobs = p.ns + p.nd;

@@ -67,8 +67,8 @@ def test_gpu_potential_field_window_golden(gpu, W):
 @pytest.mark.parametrize("ns,nd", [(13, 5), (30, 5), (0, 0), (2, 1)])
 def test_gpu_blocks_vs_oracle_rollout(gpu, ns, nd):
     """Block counts of every state along a Philox rollout with autoreset (N not a multiple of 256)
-    equal the oracle's on the same state: the default 13+5 obstacles (one load chunk of 18), 35
-    (two chunks, the last partial), none, and 3 (one mostly masked chunk)."""
+    equal the oracle's on the same state: the default 13+5 obstacles (three load chunks of 6), 35
+    (six chunks, the last partial), none, and 3 (one partial chunk)."""
     from gym_ballenv_amd import BatchedBallEnv, EnvConfig
     N = 3000
     env = BatchedBallEnv(N, 10, EnvConfig(time_limit=30, num_static=ns, num_dynamic=nd, obstacle_speed=[1] * nd),

@@ -1,0 +1,54 @@
+"""Per-region kernel averages from a rocprofv3 kernel trace (run_kernel_trace.csv) of the default
+`python3 bench.py` command: the headline's timed region, config 2's and the 2^20-env leg's.
+
+    python tools/trace_regions.py <kernel_trace.csv> [--warmup 100] [--untimed 1000] [--steps 1000]
+
+bench.py's headline leg launches the step kernel `warmup` times eagerly, replays the captured graph
+for `untimed` steps (settle), then times `steps` launches: launches warmup+untimed+1 ..
+warmup+untimed+steps of the headline kernel are the timed region.  The config-2 and large-batch legs
+are the last 1000 / 200 launches of their kernels."""
+import argparse
+import csv
+import statistics
+from collections import defaultdict
+
+ap = argparse.ArgumentParser()
+ap.add_argument("trace")
+ap.add_argument("--warmup", type=int, default=100)
+ap.add_argument("--untimed", type=int, default=1000)
+ap.add_argument("--steps", type=int, default=1000)
+a = ap.parse_args()
+
+runs = defaultdict(list)
+for r in csv.DictReader(open(a.trace)):
+    runs[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+for k in runs:
+    runs[k].sort()
+
+
+def avg_us(launches):
+    return statistics.mean((e - s) for s, e in launches) / 1e3
+
+
+def find(prefix):
+    return next((k for k in runs if k.startswith(prefix)), None)
+
+
+head = find("step2_kernel<10, 13, 5>")
+if head:
+    L = runs[head]
+    lo = a.warmup + a.untimed
+    reg = L[lo:lo + a.steps]
+    print(f"{head}: {len(L)} launches in the whole command; the headline's timed region (launches "
+          f"{lo + 1}..{lo + len(reg)}) averages {avg_us(reg):.3f} us per launch; "
+          f"65536 x 390 B / that = {65536 * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
+for prefix, last, what in (("stepw_kernel<5, 13, 5, 8>", 1000, "config 2, 4096 envs, W=5"),
+                           ("be_kernel<10, 0, 13, 5>", 200, "2^20 envs, large_batch"),
+                           ("board_kernel<6, false, 1>", 1000, "createBoard step, 65536 envs"),
+                           ("board_kernel<6, true, 1>", 10, "createBoard fused, 100 steps per launch"),
+                           ("rollout_kernel<10, 13, 5, 13, 2, 10>", 10, "config 5 fused, 100 steps per launch"),
+                           ("blocks_kernel", 200, "prep_state2 blocks (last leg size)")):
+    k = find(prefix)
+    if k:
+        L = runs[k]
+        print(f"{k} ({what}): {len(L)} launches; the last {min(last, len(L))} average {avg_us(L[-last:]):.3f} us")
