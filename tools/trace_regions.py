@@ -31,7 +31,7 @@ def avg_us(launches):
 
 
 def find(prefix):
-    return next((k for k in runs if k.startswith(prefix)), None)
+    return next((k for k in runs if prefix in k), None)
 
 
 head = find("step2_kernel<10, 13, 5>")
