@@ -616,7 +616,15 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     if (p.actions) a_pf = p.actions[r];
     else { dx_pf = p.deltas[2 * r]; dy_pf = p.deltas[2 * r + 1]; }
   };
-  if (p.mode != 1) fetch(0);
+  if (p.mode != 1) {
+    fetch(0);
+    // step 0's action lands before the loop: inside it the only pending read of a_pf is the one
+    // issued a step earlier, so its wait need not cover that step's stores (vmcnt(#stores), where a
+    // loop entered with a_pf in flight merges to vmcnt(0))
+#ifndef BE_BOARD_NO_ENTRY_WAIT   // (A/B builds)
+    if constexpr (ROLL) asm volatile("" ::"v"(a_pf), "v"(dx_pf), "v"(dy_pf));
+#endif
+  }
   for (int s = 0; s < steps; ++s) {
     const int64_t row = (int64_t)s * p.n + i;   // this step's output row (i for modes 0 / 1)
     bool do_reset = valid && p.mode == 1 && (!p.mask || p.mask[i]);
