@@ -74,6 +74,10 @@ def parse():
     p.add_argument("--config2-steps", type=int, default=1000,
                    help="BASELINE config 2 leg (4096 envs/GPU, W=5, step API): timed steps (0 = skip)")
     p.add_argument("--config2-envs", type=int, default=4096)
+    p.add_argument("--config4-steps", type=int, default=1000,
+                   help="BASELINE config 4 leg (a fixed 262144-env batch at W=10 split over the ranks, strong "
+                        "scaling): timed steps (0 = skip)")
+    p.add_argument("--config4-envs", type=int, default=262144, help="config 4: global envs over all ranks")
     p.add_argument("--large-steps", type=int, default=200,
                    help="large-batch leg (2^20 envs/GPU, W=10: past the 256-MB Infinity Cache): timed steps "
                         "(0 = skip)")
@@ -440,15 +444,20 @@ def rollout_leg(args, gb, dev, rank, world, stream):
     return res
 
 
-def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, chunk=250):
+def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, chunk=250, env_offset=None,
+                    global_envs=None):
     """be_step of N envs/GPU at window W, T steps replayed from hipGraphs of captured launches
     (the headline's method), after `settle` untimed steps since reset (0: timed straight from
-    the reset).  Returns (result dict, kernel name); the env is closed."""
+    the reset).  Envs are the global ids [env_offset, env_offset + N) (default rank * N: weak
+    scaling); `global_envs` (strong scaling: a fixed batch split over the ranks) sets the
+    env-steps counted per step and adds the ranks' combined episode statistics (all_gather).
+    Returns (result dict, kernel name); the env is closed."""
     import ctypes as C
     import torch
     from gym_ballenv_amd import _abi
     cfg = gb.EnvConfig()
-    env = gb.BatchedBallEnv(N, W, cfg, device=dev, seed=seed, env_offset=rank * N)
+    off = rank * N if env_offset is None else env_offset
+    env = gb.BatchedBallEnv(N, W, cfg, device=dev, seed=seed, env_offset=off)
     acts = env.sample_actions(T, seed=seed)
     lib, ctx, st, out = env._lib, env._ctx, C.byref(env._st), C.byref(env._out)
     graphs, cap = [], torch.cuda.Stream(dev)
@@ -476,12 +485,17 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
     el, ms = timed_graph_steps(graphs, T, dev, stream, world)
     env.status()
     kname = env.kernel_name("step")
+    episodes = None
+    if global_envs is not None:
+        per_rank = gb.gather_stats(env.stats_record()) if DIST_ON else env.stats_record().reshape(1, -1)
+        episodes = gb.combine_stats(per_rank)
     del graphs
     env.close()
     B = gb.survey_step_bytes(cfg, W)
     B_eng = gb.step_bytes(cfg, W)
     us = ms * 1e3
-    res = {"value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3, "steps": T,
+    units = N * world if global_envs is None else global_envs
+    res = {"value": T * units / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3, "steps": T,
            "untimed_steps_since_reset": untimed, "envs_per_gpu": N, "window": W, "kernel": kname,
            "kernel_us_mean": us,
            "roofline": {"bound": "hbm", "bytes_per_env_step": B, "achieved": B * N / (us * 1e-6) / 1e9,
@@ -489,6 +503,8 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
                         "engine_bytes_per_env_step": B_eng,
                         "engine_frac": B_eng * N / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                         "measured_frac": None}}
+    if episodes is not None:
+        res["episodes"] = episodes
     return res, kname
 
 
@@ -509,6 +525,27 @@ def config2_leg(args, gb, dev, rank, world, stream):
     res["workload"] = (f"BASELINE config 2: BallEnv step + prep_state4, random actions, {N} envs/GPU, W=5, 13 static "
                        "+ 5 dynamic obstacles, TimeLimit 1000, autoreset, hipGraph replay of be_step launches")
     add_measured(res["roofline"], committed_pmc("r03_pmc_config2.json", kname, N), res["kernel_us_mean"])
+    return res
+
+
+def config4_leg(args, gb, dev, rank, world, stream):
+    """BASELINE config 4: a FIXED batch of 262 144 envs at W=10, split over the ranks (strong
+    scaling; one rank per GPU): rank r steps the contiguous global ids shard(262144, r, world)
+    -- 262 144 envs at N=1, 32 768 per GPU at N=8 -- with no per-step collective; after the timed
+    region the ranks' episode records are all_gathered (RCCL) and combined.  Every env's
+    trajectory is that of the one-rank run (Philox keyed by global env id).  1000 graph-replayed
+    be_step launches per rank; value = global envs x steps / max-over-ranks wall time."""
+    from gym_ballenv_amd.distributed import shard
+    G, W = args.config4_envs, 10
+    off, n = shard(G, rank, world)
+    res, kname = graph_steps_leg(gb, dev, rank, world, stream, n, W, args.config4_steps, args.settle,
+                                 env_offset=off, global_envs=G)
+    res["workload"] = (f"BASELINE config 4: BallEnv step + prep_state4, random actions, {G} envs in total at W={W} "
+                       f"split over {world} rank(s) ({n} envs on rank {rank}), 13 static + 5 dynamic obstacles, "
+                       "TimeLimit 1000, autoreset, hipGraph replay of be_step launches; stats all_gather after the "
+                       "timed region")
+    res.update({"global_envs": G, "envs_per_rank": n, "ranks": world, "scaling": "strong"})
+    add_measured(res["roofline"], committed_pmc(f"r04_pmc_config4_{n}.json", kname, n), res["kernel_us_mean"])
     return res
 
 
@@ -834,6 +871,7 @@ def main():
 
     cold_res = cold_actions_leg(args, env, lib, dev, stream, world, B) if args.cold_steps > 0 else None
     c2_res = config2_leg(args, gb, dev, rank, world, stream) if args.config2_steps > 0 else None
+    c4_res = config4_leg(args, gb, dev, rank, world, stream) if args.config4_steps > 0 else None
     large_res = large_batch_leg(args, gb, dev, rank, world, stream) if args.large_steps > 0 else None
     fresh_res = from_reset_leg(args, gb, dev, rank, world, stream) if args.from_reset_steps > 0 else None
     pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
@@ -869,6 +907,7 @@ def main():
             "episodes": ep,
             "cold_action_rows": cold_res,
             "config2": c2_res,
+            "config4": c4_res,
             "large_batch": large_res,
             "from_reset": fresh_res,
             "policy_rollout": pol_res,

@@ -319,18 +319,30 @@ class BatchedBallEnv:
     def save_state(self, device=None) -> torch.Tensor:
         """be_save_state: every env's state packed into one u8 blob (include/ballenv.h layout:
         64-byte header, then the be_state arrays), on this env's device or ``device`` ("cpu":
-        pinned host memory).  Asynchronous on the current stream."""
+        pinned host memory).  A device blob fills asynchronously on the current stream; a host
+        blob is complete when this returns.  load_state() checks the blob's length and header,
+        and returns only after a host blob has been read."""
         n = int(self._lib.be_state_blob_bytes(C.byref(self._abi_cfg)))
         dev = self.device if device is None else torch.device(device)
         blob = torch.empty(n, dtype=torch.uint8, device=dev, pin_memory=dev.type == "cpu")
         _abi.check(self._lib.be_save_state(self._ctx, C.byref(self._st), blob.data_ptr(), self._stream()), self._ctx)
+        if dev.type == "cpu":      # a host blob is complete on return (ready for torch.save)
+            torch.cuda.current_stream(self.device).synchronize()
         return blob
 
     def load_state(self, blob: torch.Tensor) -> None:
         """be_load_state: restore every env's state from a save_state() blob (header checked)."""
         if blob.dtype != torch.uint8 or not blob.is_contiguous():
             raise ValueError("blob must be a contiguous uint8 tensor from save_state()")
+        n = int(self._lib.be_state_blob_bytes(C.byref(self._abi_cfg)))
+        if blob.numel() < n:
+            raise ValueError(f"blob holds {blob.numel()} bytes, this env's state needs {n} (truncated blob?)")
+        host = blob.device.type == "cpu"
+        if host and not blob.is_pinned():
+            blob = blob.pin_memory()
         _abi.check(self._lib.be_load_state(self._ctx, C.byref(self._st), blob.data_ptr(), self._stream()), self._ctx)
+        if host:                   # the copies have read the host blob before it can be dropped or reused
+            torch.cuda.current_stream(self.device).synchronize()
 
     def close(self) -> None:
         if self._ctx is not None:

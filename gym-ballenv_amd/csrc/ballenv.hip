@@ -42,6 +42,7 @@
 
 #include <math.h>
 #include <algorithm>
+#include <mutex>
 #include <new>
 #include <stdint.h>
 #include <stdio.h>
@@ -1659,10 +1660,14 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t x) {   // OR with the other
   return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
 }
 
-template <int WT, int NSC, int NDC>
-__global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
-  constexpr int CT = S2_CT;
-  constexpr int L = 2, EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
+// L = 4 (four lanes per env, 16 envs per wave) for the small per-GPU shards of a split batch
+// (BASELINE config 4: 32 768 envs per GPU at N = 8): one block of CT = 128 threads is 32 envs,
+// one stats slot, folded by wave 0 after a block barrier at the end (as stepw_kernel does).
+template <int WT, int NSC, int NDC, int L = 2, int CT = S2_CT>
+__global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
+  static_assert(L == 2 || L == 4, "two or four lanes per env");
+  static_assert(L == 2 || CT / L == 32, "four lanes: 32-env blocks (one stats slot)");
+  constexpr int EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
   constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;   // obstacle slots per lane
   constexpr int KR = Geo<WT>::K, F = Geo<WT>::F, NW = Geo<WT>::NW;
   constexpr int NQ = F / 8, HQ = (NQ + 1) / 2;                     // uint2 words per row / per lane
@@ -1676,8 +1681,8 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
 
   DIAG(0);
   if (DBG(DBG_EXIT_ENTRY)) return;
-  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & 1;
-  const int blk0 = (int)blockIdx.x * EPB, i = blk0 + (tid >> 1), e0 = blk0 + w * EPW;
+  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
+  const int blk0 = (int)blockIdx.x * EPB, i = blk0 + tid / L, e0 = blk0 + w * EPW;
   uint8_t* stage_blk = smem + (size_t)(SS + SD + 1) * CT * 4;   // [EPB envs][F]
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
@@ -1716,9 +1721,9 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   const int a = ld_s(p.actions, ic);
   // the wave's stats slot (one per 32 envs), read now: a wave with a finished env updates it at
   // the very end, and a dependent load there would lengthen exactly the waves that reset
-  double* const slot = p.stats ? p.stats + ((size_t)blockIdx.x * NWAVE + w) * 8 : nullptr;
+  double* const slot = p.stats ? p.stats + (size_t)(e0 / 32) * 8 : nullptr;
   double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sp2 = sp0;
-  if (slot && lane == 0 && e0 < N) {
+  if (slot && lane == 0 && e0 < N && (L == 2 || w == 0)) {
     sp0 = reinterpret_cast<const double2*>(slot)[0];
     sp1 = reinterpret_cast<const double2*>(slot)[1];
     sp2 = reinterpret_cast<const double2*>(slot)[2];
@@ -1752,7 +1757,9 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     const int k = L * j + h;
     const bool real = k < NDC;
     int ox = px(dp[j]), oy = py(dp[j]);
-    const uint32_t f = h ? pick_field(b0, min(L * j + 1, 4)) : pick_field(b0, L * j);
+    uint32_t f;
+    if constexpr (L == 2) f = h ? pick_field(b0, min(L * j + 1, 4)) : pick_field(b0, L * j);
+    else f = pick_field(b0, min(L * j + h, 4));
     uint32_t fl = 0u;
     ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[min(k, NDC - 1)], change, f, fl);
     st_flags |= real ? fl : 0u;
@@ -1791,8 +1798,8 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   for (int j = 0; j < SD; ++j) obstacle_pk(dnew[j], L * j + h < NDC, hd);
 #pragma unroll
   for (int j = 0; j < SS; ++j) obstacle_pk(so[j], L * j + h < NSC, hs);
-  hs = pair_or((uint32_t)hs) != 0u;
-  hd = pair_or((uint32_t)hd) != 0u;
+  hs = group_or<L>((uint32_t)hs) != 0u;
+  hd = group_or<L>((uint32_t)hd) != 0u;
   DIAG(10);
 
   // ---- distance, reward, done (ballenv_env.py:268-286, 200-229), on both lanes
@@ -1805,7 +1812,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   const bool trunc = p.time_limit > 0 && len >= p.time_limit;
   const bool done = env_done || trunc;
   const bool do_reset = valid && done && p.autoreset;
-  if (valid) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
+  if (valid && L == 2) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
     double* pd = h ? p.ep_return : p.reward;
     st_wt(pd + i, h ? ret : reward);
     int32_t* pi = h ? p.ep_len : p.agent;
@@ -1817,6 +1824,19 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
       if (!h && p.final_return) st_wt(p.final_return + i, ret);
       if (h && p.final_len) st_wt(p.final_len + i, len);
     }
+  } else if (valid) {   // four lanes: reward + done | ep_return + truncated | prev_dist + agent | ep_len
+    double* pd = h == 0 ? p.reward : (h == 1 ? p.ep_return : p.prev_dist);
+    if (h < 3) st_wt(pd + i, h == 0 ? reward : (h == 1 ? ret : dist));
+    if (h == 2) st_wt(p.agent + i, pk(ax, ay));
+    if (h == 3) st_wt(p.ep_len + i, len);
+    uint8_t* pb = h ? p.truncated : p.done;
+    if (pb && h < 2) st_wt(pb + i, (uint8_t)(h ? (trunc && !env_done) : done));
+    if (done) {
+      if (h == 1 && p.final_return) st_wt(p.final_return + i, ret);
+      if (h == 3 && p.final_len) st_wt(p.final_len + i, len);
+    }
+  }
+  if (valid) {
     // (stored after done is known: measured faster than storing inside the obstacle loop)
 #pragma unroll
     for (int j = 0; j < SD; ++j) {
@@ -1845,7 +1865,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     uint32_t rows[KR], flat[NW];
     raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
 #pragma unroll
-    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k]);
+    for (int k = 0; k < KR; ++k) rows[k] = group_or<L>(rows[k]);
     flatten<WT>(rows, flat);
     if (!h) write_row_global<WT>(p.terminal_obs + (int64_t)i * F, flat, quadrant(ax, ay, gx, gy));
   }
@@ -1859,15 +1879,31 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
-      if (h) return;   // both lanes take the new agent / goal / rows; lane 0 stores the scalars
-      st_wt(p.agent + i, ag);
-      st_wt(p.goal + i, go);
+      // every lane of the group takes the new agent / goal / rows; each scalar is stored by the
+      // lane that stored it in the physics above, so same-address stores stay in one lane's
+      // program order (two lanes: lane 1 ep_return / ep_len; four: lane 1 ep_return, lane 2
+      // agent / prev_dist, lane 3 ep_len)
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
-      st_wt(p.prev_dist + i, prev);
+      if constexpr (L == 2) {
+        if (h) {
+          st_wt(p.ep_return + i, 0.0);
+          st_wt(p.ep_len + i, 0);
+          return;
+        }
+        st_wt(p.agent + i, ag);
+        st_wt(p.prev_dist + i, prev);
+      } else {
+        if (h == 1) st_wt(p.ep_return + i, 0.0);
+        if (h == 3) st_wt(p.ep_len + i, 0);
+        if (h == 2) {
+          st_wt(p.agent + i, ag);
+          st_wt(p.prev_dist + i, prev);
+        }
+        if (h) return;
+      }
+      st_wt(p.goal + i, go);
       st_wt(p.total_dist + i, td);
-      st_wt(p.ep_return + i, 0.0);
-      st_wt(p.ep_len + i, 0);
       st_wt(p.episode + i, episode + 1u);
     };
     if (!(m & (m - 1)))
@@ -1886,9 +1922,25 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     uint32_t rows[KR], flat[NW];
     raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
 #pragma unroll
-    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k] | xrows[k]);
+    for (int k = 0; k < KR; ++k) rows[k] = group_or<L>(rows[k] | xrows[k]);
     flatten<WT>(rows, flat);
     const int quad = quadrant(ax, ay, gx, gy);
+    if constexpr (L == 4) {
+      // lane h writes uint2 row words [q0, q0 + nq) = [0, 4) / [4, 7) / [7, 10) / [10, 13): word q
+      // holds cells 8q-4 .. 8q+3 (word 0 starts with the quadrant one-hot); c = the lane's cells
+      // from bit 0
+      const int q0 = h == 0 ? 0 : 3 * h + 1, nq = h == 0 ? 4 : 3;
+      const uint32_t c = h == 0 ? flat[0] << 4
+                       : h == 1 ? (flat[0] >> 28) | (flat[1] << 4)
+                       : h == 2 ? (flat[1] >> 20) | (flat[2] << 12) : (flat[2] >> 12) | (flat[3] << 20);
+      auto word4 = [&](int jj) -> uint32_t { return (((c >> (4 * jj)) & 0xFu) * 0x00204081u) & 0x01010101u; };
+      uint2* dst = reinterpret_cast<uint2*>(stage + (lane >> 2) * F) + q0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t w0 = (q == 0 && h == 0) ? 1u << (8 * quad) : word4(2 * q);
+        if (q < nq) dst[q] = make_uint2(w0, word4(2 * q + 1));
+      }
+    } else {
     // uint2 word q of this lane is row word 2(q + 7h) .. +1: word j >= 1 expands cells
     // 4(j-1) .. 4(j-1)+3.  c holds this lane's cells from bit 0: lane 0 cells -4.. (its word 0
     // is the quadrant one-hot), lane 1 cells 52..
@@ -1905,9 +1957,10 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
       const uint32_t w0 = q == 0 ? (h ? word(0) : 1u << (8 * quad)) : word(2 * q);
       if (q < NQ - HQ || !h) dst[q] = make_uint2(w0, word(2 * q + 1));
     }
+    }
   }
   DIAG(4);
-  // the wave's 32 contiguous rows out (no block barrier: a wave that reset delays nobody)
+  // the wave's contiguous rows out (no block barrier: a wave that reset delays nobody)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1922,7 +1975,26 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   // the episode statistics fold after the obs stores are issued: off the path to the last store
   // (6.55 -> 6.45 us; a reset leaves this lane's ret / len registers as the finished episode's)
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
-  if (slot && !DBG(DBG_NO_STATS)) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
+  if constexpr (L == 2) {
+    if (slot && !DBG(DBG_NO_STATS)) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
+  } else {   // the block's 32 envs span both waves: through LDS, one barrier, wave 0 folds in env order
+    __shared__ uint8_t s_fin[32];
+    __shared__ double s_fret[32];
+    __shared__ int s_flen[32];
+    if (slot && !DBG(DBG_NO_STATS)) {
+      const int el = tid / L;
+      if (h == 0) {
+        s_fin[el] = (done && valid) ? 1 : 0;
+        s_fret[el] = ret;
+        s_flen[el] = len;
+      }
+      __syncthreads();
+      if (w == 0) {
+        const bool d = lane < 32 && s_fin[lane & 31];
+        if (__ballot(d)) ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
+      }
+    }
+  }
   if (slot && lane == 0 && ws.n > 0.0) {
     reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
     reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
@@ -2173,16 +2245,22 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
-      if (h) return;   // every lane of the group takes the new agent / goal / rows; lane 0 stores
-      st_wt(p.agent + i, ag);
-      st_wt(p.goal + i, go);
+      // every lane of the group takes the new agent / goal / rows; each scalar is stored by the
+      // lane that stored it in the physics above (lane 0 agent, lane 1 ep_return / ep_len, lane 2
+      // prev_dist), so same-address stores stay in one lane's program order
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
-      st_wt(p.prev_dist + i, prev);
-      st_wt(p.total_dist + i, td);
-      st_wt(p.ep_return + i, 0.0);
-      st_wt(p.ep_len + i, 0);
-      st_wt(p.episode + i, episode + 1u);
+      if (h == 0) {
+        st_wt(p.agent + i, ag);
+        st_wt(p.goal + i, go);
+        st_wt(p.total_dist + i, td);
+        st_wt(p.episode + i, episode + 1u);
+      } else if (h == 1) {
+        st_wt(p.ep_return + i, 0.0);
+        st_wt(p.ep_len + i, 0);
+      } else if (h == 2) {
+        st_wt(p.prev_dist + i, prev);
+      }
     };
     if (!(m & (m - 1)))
       wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
@@ -2994,14 +3072,25 @@ struct Launch { KFn fn; int epb; int lds; char name[48]; int threads = BLOCK_THR
 #endif
 constexpr int FIX_NS = BE_FIX_NS, FIX_ND = BE_FIX_ND;
 
-Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, bool lpe2_ok = false, int lpe5 = 0) {
+Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lanes10 = 1, int lpe5 = 0) {
   int W = c.window;
   const int F = 4 + W * W, nobs = c.num_static + c.num_dynamic;
   Launch L{nullptr, 0, 0, {0}};
   bool staged = true;
   const bool fixed = fixed_ok && mode == MODE_STEP && c.num_static == FIX_NS && c.num_dynamic == FIX_ND &&
                      c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
-  if (fixed && lpe2_ok && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
+  if (fixed && lanes10 == 4 && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
+    // four lanes per env: 16 envs per wave, 32 per 128-thread block
+    constexpr int CT4 = 128;
+    L.fn = step2_kernel<10, FIX_NS, FIX_ND, 4, CT4>;
+    L.epb = CT4 / 4;
+    L.threads = CT4;
+    constexpr int SLOTS = (FIX_NS + 3) / 4 + (FIX_ND + 3) / 4 + 1;
+    L.lds = SLOTS * CT4 * 4 + L.epb * F;
+    snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d, 4, %d>", FIX_NS, FIX_ND, CT4);
+    return L;
+  }
+  if (fixed && lanes10 == 2 && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
     // two lanes per env (step2_kernel): 32 envs per wave, 128 per block
     L.fn = step2_kernel<10, FIX_NS, FIX_ND>;
     L.epb = S2_CT / 2;
@@ -3096,12 +3185,13 @@ struct be_ctx {
   bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
-  bool step_lpe1;      // the one-lane-per-env fixed step kernel instead of step2_kernel (see below)
+  int step_lanes;      // W = 10: lanes per env of the fixed step kernel (1: be_kernel; 2 / 4: step2_kernel)
   int step5_lpe;       // W = 5: lanes per env of the fixed step kernel (1: be_kernel; 4 / 8: stepw_kernel)
   int roll5_lpe;       // W = 5: lanes per env of the fused rollout (1: rollout_kernel; 4 / 8: rolloutw_kernel)
   int max_lds;         // the device's LDS bytes per workgroup
   int64_t blob_hdr[8]; // be_save_state's header (host memory that outlives the async copy)
   mutable struct { KFn fn; int lds; bool ok; } lds_cache[4];   // fits_lds() answers per (kernel, dynamic LDS)
+  mutable std::mutex lds_mu;                                    // guards lds_cache (const entries may race)
   char err[512];
 };
 
@@ -3111,6 +3201,7 @@ struct be_ctx {
 // larger R must take the per-step fallback instead of failing the launch.
 static bool fits_lds(const be_ctx* ctx, const Launch& L) {
   if (!L.fn) return false;
+  std::lock_guard<std::mutex> lock(ctx->lds_mu);
   for (auto& c : ctx->lds_cache)
     if (c.fn == L.fn && c.lds == L.lds) return c.ok;
   hipFuncAttributes fa;
@@ -3262,7 +3353,7 @@ const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
   const bool fixed_ok = !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals;
   Launch L{nullptr, 0, 0, {0}};
   switch (entry) {
-    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, !ctx->step_lpe1, ctx->step5_lpe); break;
+    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, ctx->step_lanes, ctx->step5_lpe); break;
     case BE_ENTRY_STEP_SAMPLED: L = pick_kernel(ctx->cfg, MODE_STEP, false); break;
     case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok, ctx->roll5_lpe); if (!fits_lds(ctx, L)) L.fn = nullptr; break;
     case BE_ENTRY_RESET: L = pick_kernel(ctx->cfg, MODE_RESET, false); break;
@@ -3335,7 +3426,7 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
      // 256 CUs: step2 6.42 / 7.51 us at 65 536 / 98 304 envs against 6.97 / 7.92; one lane 8.13 /
      // 14.5 / 48.9 us at 131 072 / 262 144 / 2^20 against 8.54 / 16.2 / 52.6).
      // BALLENV_STEP_LPE=1 / 2 forces one or two lanes (A/B).
-    ctx->step_lpe1 = (int64_t)cfg->num_envs > (int64_t)96 * 4 * cus;
+    ctx->step_lanes = (int64_t)cfg->num_envs > (int64_t)96 * 4 * cus ? 1 : 2;
   }
   // W = 5 (BASELINE config 2): stepw_kernel's 8 lanes per env while one lane per env would leave
   // most of the chip idle (<= 64 envs per CU), the one-lane kernel above that.
@@ -3351,9 +3442,10 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
     else if (!strcmp(l, "4")) ctx->step5_lpe = 4;
     else if (!strcmp(l, "8")) ctx->step5_lpe = 8;
   }
-  if (const char* l = getenv("BALLENV_STEP_LPE")) {   // A/B override: exactly "1" or "2", else ignored
-    if (!strcmp(l, "1")) ctx->step_lpe1 = true;
-    else if (!strcmp(l, "2")) ctx->step_lpe1 = false;
+  if (const char* l = getenv("BALLENV_STEP_LPE")) {   // A/B override: exactly "1", "2" or "4", else ignored
+    if (!strcmp(l, "1")) ctx->step_lanes = 1;
+    else if (!strcmp(l, "2")) ctx->step_lanes = 2;
+    else if (!strcmp(l, "4")) ctx->step_lanes = 4;
   }
   if (hipDeviceGetAttribute(&ctx->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess ||
       ctx->max_lds <= 0)
@@ -3441,7 +3533,7 @@ static int launch(be_ctx* ctx, int mode, KParams& a, void* stream, int32_t steps
   int cur = -1;
   HIP_TRY(ctx, hipGetDevice(&cur));
   if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, !ctx->step_lpe1, ctx->step5_lpe);
+  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, ctx->step_lanes, ctx->step5_lpe);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)L.threads);
   for (int32_t s = 0; s < steps; ++s) {

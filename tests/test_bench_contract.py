@@ -27,7 +27,8 @@ def test_cpu_baseline_leg_small_sample():
 def test_bench_json_line(gpu):
     cmd = [sys.executable, "bench.py", "--steps", "20", "--warmup", "5", "--settle", "60", "--no-cpu-baseline",
            "--policy-steps", "20", "--torch-policy-steps", "5", "--board-steps", "20", "--rollout-steps", "100",
-           "--config2-steps", "50", "--large-steps", "20", "--from-reset-steps", "20", "--blocks-launches", "8"]
+           "--config2-steps", "50", "--config4-steps", "20", "--large-steps", "20", "--from-reset-steps", "20",
+           "--blocks-launches", "8"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -40,9 +41,12 @@ def test_bench_json_line(gpu):
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9 and rf["kernel"] == "step2_kernel<10, 13, 5>"
     assert rf["traffic"] is None or rf["traffic"] > 0
-    for leg in ("policy_rollout", "fused_rollout", "board_profile", "config2", "large_batch", "from_reset"):
+    for leg in ("policy_rollout", "fused_rollout", "board_profile", "config2", "config4", "large_batch", "from_reset"):
         assert d[leg]["value"] > 0, leg
     assert d["config2"]["envs_per_gpu"] == 4096 and d["config2"]["window"] == 5
+    c4 = d["config4"]
+    assert c4["global_envs"] == 262144 and c4["envs_per_rank"] == 262144 and c4["window"] == 10
+    assert c4["scaling"] == "strong" and c4["roofline"]["bytes_per_env_step"] == 390 and c4["episodes"]["episodes"] > 0
     assert d["config2"]["roofline"]["bytes_per_env_step"] == 315
     assert d["large_batch"]["envs_per_gpu"] == 1 << 20 and d["large_batch"]["steps"] == 20
     assert d["from_reset"]["untimed_steps_since_reset"] == 0
@@ -54,8 +58,8 @@ def test_bench_json_line(gpu):
 
 
 _ONLY_HEADLINE = ["--no-cpu-baseline", "--policy-steps", "0", "--board-steps", "0", "--rollout-steps", "0",
-                  "--cold-steps", "0", "--config2-steps", "0", "--large-steps", "0", "--from-reset-steps", "0",
-                  "--blocks-launches", "0"]
+                  "--cold-steps", "0", "--config2-steps", "0", "--config4-steps", "0", "--large-steps", "0",
+                  "--from-reset-steps", "0", "--blocks-launches", "0"]
 
 
 def _bench_line(args, timeout=110):
@@ -95,6 +99,28 @@ def test_bench_multi_rank_gloo(gpu):
 
 
 @pytest.mark.gpu
+def test_bench_config4_split_gloo(gpu):
+    """BASELINE config 4 as stated: a fixed 262 144-env batch split over the ranks.  Under
+    `--gpus 2` each rank steps its contiguous half (131 072 global ids); the leg reports the
+    global batch, and the ranks' all_gathered episodes equal those of one rank stepping the
+    whole batch (the same global ids, so the same trajectories)."""
+    only_c4 = [a for a in _ONLY_HEADLINE]
+    only_c4[only_c4.index("--config4-steps") + 1] = "20"
+    common = ["--steps", "5", "--warmup", "2", "--settle", "60", "--envs", "4096", *only_c4]
+    d2 = _bench_line(["--gpus", "2", "--dist-backend", "gloo", *common], timeout=200)
+    d1 = _bench_line(["--gpus", "1", *common], timeout=200)
+    c2, c1 = d2["config4"], d1["config4"]
+    assert c2["global_envs"] == c1["global_envs"] == 262144
+    assert c2["envs_per_rank"] == 131072 and c1["envs_per_rank"] == 262144 and c2["ranks"] == 2
+    assert c2["steps"] == c1["steps"] == 20 and c2["value"] > 0 and c1["value"] > 0
+    e1, e2 = c1["episodes"], c2["episodes"]
+    assert e1["episodes"] > 0 and e2["episodes"] == e1["episodes"]
+    assert e2["min_return"] == e1["min_return"] and e2["max_return"] == e1["max_return"]
+    assert e2["mean_return"] == pytest.approx(e1["mean_return"], rel=1e-12)
+    assert e2["mean_length"] == pytest.approx(e1["mean_length"], rel=1e-12)
+
+
+@pytest.mark.gpu
 def test_bench_rccl_one_rank(gpu):
     """The RCCL path of bench.py (the driver's torchrun form, backend nccl = RCCL): under
     torch.distributed.run with one rank the process group comes up and every collective of the
@@ -107,12 +133,14 @@ def test_bench_rccl_one_rank(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr=127.0.0.1",
            f"--master-port={port}", "bench.py", "--gpus", "1", "--dist-backend", "nccl", "--steps", "20", "--warmup", "5",
            "--settle", "60", "--rollout-steps", "100", "--policy-steps", "20", "--torch-policy-steps", "0",
-           "--board-steps", "20", "--cold-steps", "0", "--config2-steps", "20", "--large-steps", "0",
+           "--board-steps", "20", "--cold-steps", "0", "--config2-steps", "20", "--config4-steps", "20",
+           "--large-steps", "0",
            "--from-reset-steps", "0", "--blocks-launches", "0", "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110,
                        env=dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["ranks"] == 1 and d["n_gpus"] == 1 and d["value"] > 0 and d["episodes"]["episodes"] >= 0
-    for leg in ("policy_rollout", "fused_rollout", "board_profile", "config2"):
+    for leg in ("policy_rollout", "fused_rollout", "board_profile", "config2", "config4"):
         assert d[leg]["value"] > 0, leg
+    assert d["config4"]["global_envs"] == 262144 and d["config4"]["episodes"]["episodes"] > 0

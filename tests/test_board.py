@@ -62,6 +62,36 @@ def test_oracle_board_golden(prefix):
         check_features(f, g["feat"][:, t], f"t={t}")
 
 
+@pytest.mark.parametrize("prefix", ["a", "b"])
+def test_py_board_golden(prefix):
+    """oracle/py_board.py, the scalar createBoard port timed as the board leg's CPU baseline,
+    replays the reference's own episodes: the same reset draws give the same spawns, and every
+    step the same reward, done, agent, distance, return and 20 features."""
+    from oracle.py_board import ACTIONS, PyBoard, _Draws
+    g = fixture(prefix)
+    E, T = g["actions"].shape
+    ns = g["init_static"].shape[1]
+    for e in range(E):
+        b = PyBoard(ns)
+        b.reset(_Draws(g["reset_tape"][e, : int(g["reset_used"][e])]))
+        assert b.state[0] == tuple(g["init_agent"][e]) and b.state[1] == tuple(g["init_goal"][e])
+        assert b.state[2] == g["init_dist"][e] and b.total_distance == g["init_total"][e]
+        assert [(o.x, o.y) for o in b.obstacle_list] == [tuple(p) for p in g["init_static"][e]]
+        check_features(b.sensor_readings, g["init_feat"][e], f"e={e} reset")
+        for t in range(T):
+            state, r, d = b.step(ACTIONS[g["actions"][e, t]])
+            assert r == g["reward"][e, t] and d == bool(g["done"][e, t]), (e, t)
+            assert state[0] == tuple(g["agent"][e, t]) and state[2] == g["dist"][e, t], (e, t)
+            assert b.total_reward_accumulated == g["ep_return"][e, t], (e, t)
+            check_features(b.sensor_readings, g["feat"][e, t], f"e={e} t={t}")
+
+
+def test_py_board_baseline_runs():
+    from oracle import py_board
+    n, el = py_board.run_baseline(0.2, seed=3)
+    assert n > 0 and el > 0
+
+
 def make_board(gpu, n, ns, **kw):
     from gym_ballenv_amd import BatchedBoard
     return BatchedBoard(n, ns, device=gpu, **kw)

@@ -412,9 +412,36 @@ def test_save_load_state_blob_round_trip(gpu):
         got = np_state(env)
         for k in KEYS:
             np.testing.assert_array_equal(got[k], end[k], err_msg=k)
-    other = make_env(EnvConfig(time_limit=25), N + 32, W, gpu, seed=21)
+    other = make_env(EnvConfig(time_limit=25), N - 32, W, gpu, seed=21)
     with pytest.raises(BallEnvError, match="header"):
         other.load_state(dev_blob)
+    with pytest.raises(ValueError, match="truncated"):
+        env.load_state(host_blob[: host_blob.numel() - 16])
     env.status()
     env.close()
     other.close()
+
+
+@pytest.mark.gpu
+def test_save_state_host_blob_through_torch_save(gpu, tmp_path):
+    """A host blob goes straight to torch.save with no manual synchronize (save_state returns it
+    complete), and a blob loaded back from disk -- pageable memory, dropped right after
+    load_state -- restores the state bit for bit."""
+    from gym_ballenv_amd.config import EnvConfig
+    N, W = 2048, 10
+    env = make_env(EnvConfig(), N, W, gpu, seed=33)
+    env.reset()
+    acts = env.sample_actions(30, seed=9)
+    for t in range(15):
+        env.step(acts[t])
+    want = np_state(env)
+    path = tmp_path / "state.pt"
+    torch.save(env.save_state("cpu"), path)
+    for t in range(15, 30):
+        env.step(acts[t])
+    env.load_state(torch.load(path, weights_only=True))
+    got = np_state(env)
+    for k in KEYS:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    env.status()
+    env.close()
