@@ -52,6 +52,9 @@ def parse():
                         "hipGraph replay of captured be_step launches; eager: one ctypes be_step call per step")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--cpu-procs", type=int, default=0, help="0 = one per usable host core")
+    p.add_argument("--board-cpu-seconds", type=float, default=6.0,
+                   help="createBoard CPU baseline (oracle/py_board.py on every host core) beside the board leg "
+                        "(0 = skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph-chunk", type=int, default=250, help="steps per captured graph")
     p.add_argument("--settle", type=int, default=400,
@@ -160,6 +163,30 @@ def cpu_baseline(window, seconds, procs=None):
                       f"and at W=10: single-env BallEnv.step + prep_state4, 13 static + 5 dynamic obstacles, "
                       f"uniform random 9-way actions, reset on done/1000 steps (oracle/py_ballenv.py, pure "
                       f"Python); value = W={window if window in by_w else 10} aggregate"}
+
+
+def board_cpu_baseline(seconds, procs=None, static_obstacles=6):
+    """The createBoard profile on the host cores (north_star's "reference single-env
+    pygame step() timed on the box's own host cores"): oracle/py_board.py, the scalar port of
+    createBoard.step + featureExtractor (ballenv_pygame.py:650-706, featureExtractor.py:247-265),
+    single env per process, one process per usable core, random actionArray moves, reset on
+    done / 1000 steps -- the board leg's workload (6 statics).  Checked within +-25 % of the
+    reference's own speed in the build container (tools/cpu_port_speed.py,
+    profiles/r04_cpu_port_speed.json).  No GPU is touched."""
+    from oracle import py_board
+    import multiprocessing as mp
+    cores = host_cores() if not procs else min(procs, host_cores())
+    with mp.get_context("fork").Pool(cores) as pool:
+        res = pool.map(py_board._worker, [(seconds, 2000 + i, static_obstacles) for i in range(cores)])
+    steps = sum(s for s, _ in res)
+    el = max(t for _, t in res)
+    rates = [s / t for s, t in res]
+    return {"value": steps / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "per_core": sum(rates) / len(rates), "per_core_min": min(rates), "per_core_max": max(rates),
+            "env_steps": steps, "seconds": el,
+            "sample": f"{cores} procs (one per usable core) x {seconds:.0f} s: single-env createBoard.step + "
+                      f"featureExtractor, {static_obstacles} static obstacles, random actionArray moves, reset on "
+                      "done / 1000 steps (oracle/py_board.py, pure Python + numpy)"}
 
 
 def timed_graph_steps(graphs, steps, dev, stream, world):
@@ -727,9 +754,11 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU: "
                          f"torchrun --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}, or bench.py --gpus N alone)")
 
-    base = None
+    base = board_base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base = cpu_baseline(args.window, args.cpu_seconds, args.cpu_procs)
+        if args.board_steps > 0 and args.board_cpu_seconds > 0:
+            board_base = board_cpu_baseline(args.board_cpu_seconds, args.cpu_procs)
 
     import torch
     import torch.distributed as dist
@@ -876,6 +905,8 @@ def main():
     fresh_res = from_reset_leg(args, gb, dev, rank, world, stream) if args.from_reset_steps > 0 else None
     pol_res = policy_leg(args, gb, dev, rank, world, stream) if args.policy_steps > 0 else None
     board_res = board_leg(args, gb, dev, rank, world, stream) if args.board_steps > 0 else None
+    if board_res is not None:
+        board_res["cpu_baseline"] = board_base
     roll_res = rollout_leg(args, gb, dev, rank, world, stream) if args.rollout_steps > 0 else None
     blocks_res = blocks_leg(args, gb, dev, rank, world, stream) if args.blocks_launches > 0 else None
 

@@ -30,7 +30,7 @@ BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math
 # the kernels with MFMAs (the policy forward and the fused policy rollouts) change.
 VGPR_MFMA = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 UNITS = {"ballenv.hip": VGPR_MFMA, "policy.hip": ["-fno-slp-vectorize", *VGPR_MFMA], "features.hip": [], "board.hip": []}
-HEADERS = [HDR, os.path.join(CSRC, "philox.h"), os.path.join(CSRC, "internal.h"), os.path.join(CSRC, "policy_core.h")]
+HEADERS = [HDR, *(os.path.join(CSRC, h) for h in ("philox.h", "internal.h", "policy_core.h", "diag.h"))]
 
 
 def _stale(out, deps):

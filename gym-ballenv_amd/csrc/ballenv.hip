@@ -115,52 +115,10 @@ struct KParams {
   unsigned long long pol_seed;
 };
 
-// Diagnostic phase-skip bits (timing ablations only; outputs are wrong when set).  Only
-// diagnostics builds (-DBE_DIAG_STAMPS or -DBE_DIAG_SKIP) read them; in production DBG(x) is 0.
-enum : uint32_t { DBG_NO_STATS = 1, DBG_NO_RASTER = 2, DBG_NO_OBS = 4, DBG_NO_PHILOX = 8, DBG_NO_DYN = 16,
-                  DBG_NO_NEAR = 32, DBG_EXIT_ENTRY = 64, DBG_EXIT_BARRIER = 128, DBG_EXIT_PHYSICS = 256,
-                  DBG_EXIT_RASTER = 512, DBG_WAIT_LOADS = 1024,
-                  // fused policy rollout: every env on the table / no select_action tail / no block barriers
-                  DBG_POL_TABLE = 2048, DBG_POL_NO_FINISH = 4096, DBG_POL_NO_SYNC = 8192,
-                  DBG_NO_RESET = 16384, DBG_NO_COPY = 32768 };
-#if defined(BE_DIAG_STAMPS) || defined(BE_DIAG_SKIP)
-#define DBG(x) (p.dbg & (x))
-#else
-#define DBG(x) 0
-#endif
-
-// Diagnostics-only build (-DBE_DIAG_STAMPS): per-wave phase stamps for tools/microbench.
-#ifdef BE_DIAG_STAMPS
-constexpr int DIAG_WAVES = 1 << 16, DIAG_POINTS = 16;
-__device__ unsigned long long g_diag_rt[DIAG_WAVES][DIAG_POINTS];   // s_memrealtime (100 MHz, chip-wide)
-__device__ unsigned long long g_diag_cy[DIAG_WAVES][DIAG_POINTS];   // s_memtime (shader clock)
-__device__ unsigned int g_diag_hw[DIAG_WAVES];                       // HW_ID (cu/sh/se) | XCC_ID << 28
-__device__ __forceinline__ void diag_stamp(int point) {
-  const int w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64);
-  if (point == 0 && (threadIdx.x & 63) == 0 && w < DIAG_WAVES)
-    g_diag_hw[w] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0x0FFFFFFFu |
-                   ((unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 28);
-  if ((threadIdx.x & 63) == 0 && w < DIAG_WAVES) {
-    g_diag_rt[w][point] = __builtin_amdgcn_s_memrealtime();
-    g_diag_cy[w][point] = __builtin_amdgcn_s_memtime();
-  }
-}
-#define DIAG(pt) diag_stamp(pt)
-// per-phase cycle accumulators of a multi-step kernel: PH_INIT once, PH(k) at the end of phase k
-// (adds the cycles since the previous PH), PH_STORE at the end -> g_diag_cy[wave][k]
-#define PH_INIT unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ph_t = __builtin_amdgcn_s_memtime()
-#define PH(k) do { const unsigned long long ph_n = __builtin_amdgcn_s_memtime(); ph_acc[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
-#define PH_STORE do { \
-    const int ph_w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64); \
-    if ((threadIdx.x & 63) == 0 && ph_w < DIAG_WAVES) \
-      for (int ph_k = 0; ph_k < 8; ++ph_k) g_diag_cy[ph_w][ph_k] = ph_acc[ph_k]; \
-  } while (0)
-#else
-#define DIAG(pt) ((void)0)
-#define PH_INIT ((void)0)
-#define PH(k) ((void)0)
-#define PH_STORE ((void)0)
-#endif
+// Diagnostics hooks (DBG skip bits, DIAG / PH phase stamps): no-ops in the release build; a
+// -DBE_DIAG_STAMPS / -DBE_DIAG_SKIP build (tools/build_diag.sh, tools/build_ab_lib.sh) defines them.
+#define BE_DIAG_UNIT_STEP 1
+#include "diag.h"
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ int px(int32_t p) { return (int)(int16_t)(p & 0xFFFF); }
@@ -180,23 +138,16 @@ __device__ __forceinline__ T ld_s(const T* base, uint32_t idx) {
 }
 // Output / state stores of the fixed-shape step kernels: write-through (sc1, a relaxed agent-scope
 // atomic store), so the stores drain while the wave runs instead of in the kernel-end L2 write-back.
-#ifndef BE_WT
-#define BE_WT 1
-#endif
 #ifndef BE_S2_CT
 #define BE_S2_CT 256        // step2_kernel: threads per block (A/B)
 #endif
 constexpr int S2_CT = BE_S2_CT;
-#ifndef BE_RO_STORE
-#define BE_RO_STORE 0   // the fused rollouts' per-step obs rows: plain stores (A/B builds: 1 = sc1)
-#endif
+// copy-out store kinds: the step kernels write through (sc1); the fused rollouts' per-step obs rows
+// are plain stores (sc1 there measured no faster)
+constexpr int ST_PLAIN = 0, ST_WT = 1;
 template <class T>
 __device__ __forceinline__ void st_wt(T* p, T v) {
-#if BE_WT
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  *p = v;
-#endif
 }
 template <class T>
 __device__ __forceinline__ T& ld_s_ptr(T* base, uint32_t idx) {   // (stores: the same addressing)
@@ -437,15 +388,11 @@ __device__ __forceinline__ void stage_row(uint8_t* stage, int tid, const uint32_
 }
 
 // Copy the block's staged rows to obs (u8) and/or obs_f32 with 16-byte stores.
-// BE_OBS_STORE: 1 (default) sc1 write-through buffer stores -- the kernel-end L2 write-back then has
-// little left to do (measured 7.8 -> 7.3 us per step at 65 536 envs); 0 plain, 2 nt (A/B builds).
-#ifndef BE_OBS_STORE
-#define BE_OBS_STORE 1
-#endif
-#ifndef BE_OBS_AUX
-#define BE_OBS_AUX 16   // copy_wave_full's cache-policy bits at BE_OBS_STORE 1 (gfx950: sc0 1, nt 2, sc1 16)
-#endif
-template <int BLOCK, int SF = BE_OBS_STORE>
+// SF = ST_WT (default): sc1 write-through buffer stores -- the kernel-end L2 write-back then has
+// little left to do (measured 7.8 -> 7.3 us per step at 65 536 envs; plain and nt stores slower);
+// ST_PLAIN: plain stores (the fused rollouts).
+constexpr int AUX_SC1 = 16;   // buffer-store cache-policy bits (gfx950: sc0 1, nt 2, sc1 16)
+template <int BLOCK, int SF = ST_WT>
 __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid, int64_t row0,
                                          uint8_t* obs, float* obs_f32, int tid = (int)threadIdx.x) {
   if constexpr (BLOCK == 64) {   // a wave's own rows: row0 / nvalid are wave-uniform -- say so, or the
@@ -457,18 +404,14 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid
   if (obs) {
     uint8_t* dst = obs + row0 * F;
     const int nv = bytes >> 4;
-    if constexpr (SF == 1) {
+    if constexpr (SF == ST_WT) {
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, bytes, 0x00020000);
     for (int v = tid; v < nv; v += BLOCK) {
       const uint4 x = reinterpret_cast<const uint4*>(stage)[v];
       typedef int v4i_ __attribute__((ext_vector_type(4)));
       const v4i_ y = {(int)x.x, (int)x.y, (int)x.z, (int)x.w};
-      __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v * 16, 0, 16);   // aux 16 = sc1
+      __builtin_amdgcn_raw_buffer_store_b128(y, rsrc, v * 16, 0, AUX_SC1);
     }
-    } else if constexpr (SF == 2) {
-    typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
-    for (int v = tid; v < nv; v += BLOCK)
-      __builtin_nontemporal_store(reinterpret_cast<const v4u_*>(stage)[v], reinterpret_cast<v4u_*>(dst) + v);
     } else {
     for (int v = tid; v < nv; v += BLOCK)
       reinterpret_cast<uint4*>(dst)[v] = reinterpret_cast<const uint4*>(stage)[v];
@@ -489,7 +432,7 @@ __device__ __forceinline__ void copy_out(const uint8_t* stage, int F, int nvalid
 
 // A wave's NV16 staged 16-byte words to dst (wave-uniform) in one unrolled pass: every LDS read
 // is issued before the first store, so the copy pays one LDS latency instead of one per word.
-template <int NV16, int SF = BE_OBS_STORE>
+template <int NV16, int SF = ST_WT>
 __device__ __forceinline__ void copy_wave_full(const uint8_t* stage, uint8_t* dst, int lane) {
   constexpr int IT = (NV16 + 63) / 64;
   typedef int v4i_ __attribute__((ext_vector_type(4)));
@@ -500,7 +443,7 @@ __device__ __forceinline__ void copy_wave_full(const uint8_t* stage, uint8_t* ds
   // stores of lanes past the end (no divergent second copy of the store sequence)
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, NV16 * 16, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < IT; ++j) __builtin_amdgcn_raw_buffer_store_b128(x[j], rsrc, (lane + 64 * j) * 16, 0, SF == 1 ? BE_OBS_AUX : 0);
+  for (int j = 0; j < IT; ++j) __builtin_amdgcn_raw_buffer_store_b128(x[j], rsrc, (lane + 64 * j) * 16, 0, SF == ST_WT ? AUX_SC1 : 0);
 }
 
 // Generic-W (runtime W, no staging) obs writer: per cell over the near list.
@@ -531,9 +474,6 @@ __device__ void write_row_generic(const NearList<BLOCK>& nl, const Win& g, int q
 template <int BLOCK>
 __device__ void reset_env(const KParams& p, const Tables& t, int i, ResetDraws& ds, int& ax, int& ay, int& gx,
                           int& gy, NearList<BLOCK>& nl) {
-#ifdef BE_DIAG_NO_RESET
-  (void)p; (void)t; (void)i; (void)ds; ax = ay = gx = gy = 0; nl.cnt = 0; return;
-#endif
   const int N = p.n, W = p.screen_w, H = p.screen_h;
   gx = ds.draw(W - t.strip_goal_x, W);                                  // :115
   gy = ds.draw(H - t.strip_goal_y, H);                                  // :116
@@ -692,9 +632,6 @@ __device__ __forceinline__ void wave_stats2(bool done, double ret, int len, Wave
 // ------------------------------------------------------------------ lane groups
 // LPE lanes cooperate on one env: obstacle k belongs to lane k % LPE, obs word w to lane w % LPE.
 constexpr int BLOCK_THREADS = 256;
-#ifndef BE_LPE
-#define BE_LPE 1
-#endif
 template <int LPE>
 __device__ __forceinline__ uint32_t group_or(uint32_t x) {
   static_assert(LPE == 1 || LPE == 2 || LPE == 4, "LPE must be 1, 2 or 4");
@@ -709,7 +646,7 @@ __device__ __forceinline__ int group_bcast(int x) {  // value of the group's lan
   else return __builtin_amdgcn_update_dpp(0, x, 0x00, 0xF, 0xF, false);                          // quad_perm 0,0,0,0
 }
 
-constexpr int lanes_for(int WT) { return WT == 0 ? 1 : BE_LPE; }
+constexpr int lanes_for(int) { return 1; }   // the generic kernel: one lane per env
 constexpr int envs_per_block(int WT) { return BLOCK_THREADS / lanes_for(WT); }
 constexpr int RCAP = 64;  // resets handled per cooperative pass (more loop)
 
@@ -1038,15 +975,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   uint32_t st_flags = 0;   // BE_STATUS_* raised by this lane, published once per wave
   // fixed-shape kernels defer the step's state / output stores to the very end of the wave
   // (a store still in flight makes later register reuse wait for vmcnt(0), on the critical path)
-#ifndef BE_DEFER_STORES
-#define BE_DEFER_STORES 0   // measured neutral; kept as a diagnostics switch
-#endif
-  constexpr bool DEFER = FIXED && BE_DEFER_STORES;
-  constexpr int DN = FIXED ? NDC : 1;
-  int32_t dfr_dyn[DN];
-  int dfr_goal[DN];
-  bool dfr_change = false, dfr_trunc = false;
-  double dfr_reward = 0.0, dfr_dist = 0.0;
   const uint32_t gid = (uint32_t)p.gid0 + (uint32_t)i;
 
   // ---- phase 0: issue every load of this env (independent, coalesced across the wave)
@@ -1209,12 +1137,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
           int ox = px(dp[j]), oy = py(dp[j]);
           ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[j], change, wj[j], st_flags);
           const int32_t npk = pk(ox, oy);
-          dfr_dyn[j % DN] = npk; dfr_goal[j % DN] = ngs[j];
-          if (!DEFER && valid) st_wt(p.dyn_obs + (size_t)j * N + i, npk);
+          if (valid) st_wt(p.dyn_obs + (size_t)j * N + i, npk);
           obstacle_pk(npk, hd);
         }
-        dfr_change = change;   // every obstacle re-picks its goal on the same step
-        if (!DEFER && valid && change) {
+        if (valid && change) {   // every obstacle re-picks its goal on the same step
 #pragma unroll
           for (int j = 0; j < NDC; ++j) st_wt(p.dyn_goal + (size_t)j * N + i, (uint8_t)ngs[j]);
         }
@@ -1287,8 +1213,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const bool env_done = (dist < p.threshold_goal) || hs || hd;
       const bool trunc = p.time_limit > 0 && len >= p.time_limit;
       done = env_done || trunc;
-      dfr_reward = reward; dfr_dist = dist; dfr_trunc = trunc && !env_done;
-      if (!DEFER && lead) {
+      if (lead) {
         st_wt(p.reward + i, reward);
         st_wt(p.done + i, (uint8_t)done);
         if (p.truncated) st_wt(p.truncated + i, (uint8_t)(trunc && !env_done));
@@ -1477,27 +1402,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const int e0 = blk0 + w * 64;
       DIAG(5);
       copy_out<64>(stage + w * 64 * F, F, max(0, min(64, N - e0)), (int64_t)e0, p.obs, p.obs_f32, lane);
-      if (DEFER && valid) {   // the deferred per-env stores (a reset env's state was written by wave_resets)
-        p.reward[i] = dfr_reward;
-        p.done[i] = (uint8_t)done;
-        if (p.truncated) p.truncated[i] = (uint8_t)dfr_trunc;
-        if (done) {
-          if (p.final_return) p.final_return[i] = fin_ret;
-          if (p.final_len) p.final_len[i] = fin_len;
-        }
-        if (!do_reset) {
-          p.agent[i] = pk(ax, ay);
-          p.prev_dist[i] = dfr_dist;
-          p.ep_return[i] = fin_ret;
-          p.ep_len[i] = fin_len;
-#pragma unroll
-          for (int j = 0; j < DN; ++j) (p.dyn_obs + (size_t)j * N)[i] = dfr_dyn[j];
-          if (dfr_change) {
-#pragma unroll
-            for (int j = 0; j < DN; ++j) (p.dyn_goal + (size_t)j * N)[i] = (uint8_t)dfr_goal[j];
-          }
-        }
-      }
       if (p.stats && (lane == 0 || lane == 32)) {
         const WaveStats& v = lane == 0 ? ws : ws_hi;
         if (v.n > 0.0) {
@@ -2298,10 +2202,10 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
       const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.obs + (size_t)e0u * F, (short)0, WB, 0x00020000);
       if constexpr (WB % 16 == 0) {
         const v4i_ x = reinterpret_cast<const v4i_*>(stage)[min(lane, WB / 16 - 1)];
-        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, lane * 16, 0, BE_OBS_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rsrc, lane * 16, 0, AUX_SC1);
       } else {
         const v2i_ x = reinterpret_cast<const v2i_*>(stage)[min(lane, WB / 8 - 1)];
-        __builtin_amdgcn_raw_buffer_store_b64(x, rsrc, lane * 8, 0, BE_OBS_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(x, rsrc, lane * 8, 0, AUX_SC1);
       }
     } else {   // a partial last wave, or f32 obs: byte by byte
       const int nb = max(0, min(EPW, N - e0u)) * F;
@@ -2992,9 +2896,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (nrows == 64)   // a full wave (wave-uniform): one unrolled pass, reads ahead of stores
-        copy_wave_full<64 * F / 16, BE_RO_STORE>(stage, p.obs + (so_n + (size_t)__builtin_amdgcn_readfirstlane(e0)) * F, lane);
+        copy_wave_full<64 * F / 16, ST_PLAIN>(stage, p.obs + (so_n + (size_t)__builtin_amdgcn_readfirstlane(e0)) * F, lane);
       else
-        copy_out<64, BE_RO_STORE>(stage, F, nrows, (int64_t)e0, p.obs + so_n * F, nullptr, lane);
+        copy_out<64, ST_PLAIN>(stage, F, nrows, (int64_t)e0, p.obs + so_n * F, nullptr, lane);
       // the next step's stage writes must follow this step's stage reads (LDS ops issue in order)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -3029,9 +2933,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (nrows == 64)
-      copy_wave_full<64 * F / 16, BE_RO_STORE>(stage, p.obs_last + (size_t)__builtin_amdgcn_readfirstlane(e0) * F, lane);
+      copy_wave_full<64 * F / 16, ST_PLAIN>(stage, p.obs_last + (size_t)__builtin_amdgcn_readfirstlane(e0) * F, lane);
     else
-      copy_out<64, BE_RO_STORE>(stage, F, nrows, (int64_t)e0, p.obs_last, nullptr, lane);
+      copy_out<64, ST_PLAIN>(stage, F, nrows, (int64_t)e0, p.obs_last, nullptr, lane);
   }
   if (slot && (lane & 31) == 0) {
     slot[0] = acc.n; slot[1] = acc.s1; slot[2] = acc.s2; slot[3] = acc.sl; slot[4] = acc.mn; slot[5] = acc.mx;
@@ -3066,11 +2970,7 @@ KFn kernel_for(int mode) {
 struct Launch { KFn fn; int epb; int lds; char name[48]; int threads = BLOCK_THREADS; };
 
 // Fixed-shape step kernels for the reference's default obstacle counts (ball_cnn_ac3.py:40-41).
-#ifndef BE_FIX_NS            // the reference's obstacle counts; other values only in diagnostics builds
-#define BE_FIX_NS 13
-#define BE_FIX_ND 5
-#endif
-constexpr int FIX_NS = BE_FIX_NS, FIX_ND = BE_FIX_ND;
+constexpr int FIX_NS = 13, FIX_ND = 5;   // the reference's obstacle counts (ball_cnn_ac3.py:40-41)
 
 Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lanes10 = 1, int lpe5 = 0) {
   int W = c.window;
@@ -3242,22 +3142,7 @@ extern "C" {
 
 int be_abi_version(void) { return BE_ABI_VERSION; }
 
-#ifdef BE_DIAG_STAMPS
-// diagnostics build only: copy the stamp tables out (rt, cy: DIAG_WAVES x DIAG_POINTS each)
-int be_diag_stamps(unsigned long long* rt, unsigned long long* cy) {
-  if (hipMemcpyFromSymbol(rt, HIP_SYMBOL(g_diag_rt), sizeof(g_diag_rt)) != hipSuccess) return BE_E_HIP;
-  if (hipMemcpyFromSymbol(cy, HIP_SYMBOL(g_diag_cy), sizeof(g_diag_cy)) != hipSuccess) return BE_E_HIP;
-  return BE_OK;
-}
-int be_diag_hwid(unsigned int* hw) {
-  return hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_diag_hw), sizeof(g_diag_hw)) == hipSuccess ? BE_OK : BE_E_HIP;
-}
-int be_diag_clear(void) {
-  static unsigned long long zero[DIAG_WAVES][DIAG_POINTS];
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_rt), zero, sizeof(zero)) != hipSuccess) return BE_E_HIP;
-  return BE_OK;
-}
-#endif
+BE_DIAG_STEP_ENTRIES   // diagnostics builds only (diag.h)
 
 int be_config_default(be_config* c, int32_t num_envs, int32_t window) {
   if (!c) return fail(nullptr, BE_E_INVALID, "%s", "cfg is NULL");

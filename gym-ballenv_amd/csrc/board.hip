@@ -51,25 +51,9 @@ namespace {
 
 constexpr uint32_t PURPOSE_BOARD_RESET = 6;
 
-// Diagnostics-only build (-DBE_DIAG_STAMPS): per-wave cycles per phase (s_memtime deltas summed over
-// a launch), read with be_board_diag_stamps; BPH(k) closes phase k.
-#ifdef BE_DIAG_STAMPS
-constexpr int BDIAG_WAVES = 1 << 14;
-__device__ unsigned long long g_bdiag[BDIAG_WAVES][8];
-#define BPH_INIT unsigned long long bph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bph_t = __builtin_amdgcn_s_memtime()
-#define BPH(k) do { const unsigned long long bph_n = __builtin_amdgcn_s_memtime(); bph_acc[k] += bph_n - bph_t; bph_t = bph_n; } while (0)
-#define BCOUNT(k, v) (bph_acc[k] += (unsigned long long)(v))   // counts (not cycles) in slots 5..7
-#define BPH_STORE do { \
-    const int bph_w = (int)(blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64); \
-    if ((threadIdx.x & 63) == 0 && bph_w < BDIAG_WAVES) \
-      for (int bph_k = 0; bph_k < 8; ++bph_k) g_bdiag[bph_w][bph_k] = bph_acc[bph_k]; \
-  } while (0)
-#else
-#define BPH_INIT ((void)0)
-#define BPH(k) ((void)0)
-#define BCOUNT(k, v) ((void)0)
-#define BPH_STORE ((void)0)
-#endif
+// diagnostics hooks (BPH phase stamps, BCOUNT): no-ops in the release build (diag.h)
+#define BE_DIAG_UNIT_BOARD 1
+#include "diag.h"
 constexpr int BOARD_REJECT_LIMIT = 4096;
 constexpr double PI = 3.141592653589793;   // math.pi
 
@@ -100,12 +84,6 @@ __device__ __forceinline__ double dist2(double x1, double y1, double x2, double 
 // atomic store; the features as sc1 buffer stores), so they drain while the wave runs instead of in
 // the kernel-end L2 write-back -- as the step kernels of ballenv.hip do: 8.75 -> 8.22 us per step at
 // 65 536 envs; the fused rollout too (3.68 -> 3.62 us per step; profiles/r03_board_wt_ab.txt).
-#ifndef BE_BOARD_WT
-#define BE_BOARD_WT 1
-#endif
-#ifndef BE_BOARD_WT_ROLL
-#define BE_BOARD_WT_ROLL 1
-#endif
 template <bool WT, class T>
 __device__ __forceinline__ void bst(T* p, T v) {
   if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -179,9 +157,7 @@ __device__ void features(const BParams& p, float4* out, double ax, double ay, do
   // only a wave with such a lane (never seen in practice) evaluates hypot.
   const double tq = nv / 5.0, tf = floor(tq);
   double dg = tf;
-#ifndef BE_BOARD_ALWAYS_HYPOT   // (A/B builds)
   if (tq - tf < 1e-9 || tf + 1.0 - tq < 1e-9)
-#endif
     dg = floor(hypot(ax - gx, ay - gy) / 5.0);
   f[0] = (float)(dg > 5.0 ? 5.0 : dg);
   // relativeGoalPos (:146-166): angle between (0, 1) and (gx - ax, gy - ay), acos(c) of the
@@ -192,9 +168,7 @@ __device__ void features(const BParams& p, float4* out, double ax, double ay, do
   constexpr double COS_PI4 = 0.70710678118654752;
   int bin;   // 0: ang < pi/4, 1: pi/4 < ang < 3 pi/4, 2: otherwise
   bin = c > COS_PI4 ? 0 : (c > -COS_PI4 ? 1 : 2);
-#ifndef BE_BOARD_ALWAYS_ACOS    // (A/B builds)
   if (fabs(fabs(c) - COS_PI4) < 1e-9)
-#endif
   {
     const double ang = acos(c);
     bin = ang < PI / 4 ? 0 : ((ang > PI / 4 && ang < PI * 3 / 4) ? 1 : 2);
@@ -217,11 +191,7 @@ __device__ void features(const BParams& p, float4* out, double ax, double ay, do
     c11 += real ? 1.f : 0.f;                               // orientation bin 1, speed bin 0
     // a*exp(-N/b)*N*thrPart, a = 1, b = 10; -N*0.1 is within an ulp of -N/10 (exp's own
     // accuracy class; only sf's f32 value and its > 1 cut, a measure-zero boundary, see it)
-#ifdef BE_BOARD_DIAG_NOEXP     // diagnostics (timing placebo, wrong features)
-    const double fsoc = (1.0 - N * 0.1) * N * 1.5;
-#else
     const double fsoc = exp(N * -0.1) * N * 1.5;
-#endif
     tk[j] = (real && fsoc > 1.0) ? fsoc : 0.0;             // -> phi_SF[orientation bin 1]
   }
   double sf = 0.0;
@@ -551,7 +521,7 @@ __device__ __forceinline__ void copy_feat(const float4* stage, float* dst, int n
 template <int MAXS, bool ROLL, int L>
 __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   constexpr int SPL = (MAXS + L - 1) / L, EPW = 64 / L;
-  constexpr bool WT = ROLL ? (BE_BOARD_WT_ROLL != 0) : (BE_BOARD_WT != 0);
+  constexpr bool WT = true;   // write-through in both kernels (profiles/r03_board_wt_ab.txt)
   __shared__ float4 s_feat[4][EPW * 5];   // per wave: its envs' feature rows
   const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
   float4* fstage = &s_feat[w][0];
@@ -621,9 +591,7 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     // step 0's action lands before the loop: inside it the only pending read of a_pf is the one
     // issued a step earlier, so its wait need not cover that step's stores (vmcnt(#stores), where a
     // loop entered with a_pf in flight merges to vmcnt(0))
-#ifndef BE_BOARD_NO_ENTRY_WAIT   // (A/B builds)
     if constexpr (ROLL) asm volatile("" ::"v"(a_pf), "v"(dx_pf), "v"(dy_pf));
-#endif
   }
   for (int s = 0; s < steps; ++s) {
     const int64_t row = (int64_t)s * p.n + i;   // this step's output row (i for modes 0 / 1)
@@ -678,11 +646,9 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       if (m0) {
         const uint32_t g = (uint32_t)p.gid0 + (uint32_t)i;
         unsigned long long m = m0;
-#ifndef BE_BOARD_NO_FAST_RESET   // (A/B builds: the general passes only)
         if constexpr (MAXS <= 12) {   // one Philox chain per reset; the rare rest take the general passes
           if (p.ns >= 1) m = wave_board_resets_fast<MAXS>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
         }
-#endif
         BCOUNT(5, __popcll(m0));
         BCOUNT(6, __popcll(m));
         if (m) {   // several finished envs: 2 or 4 per pass (ns must fit a slot: ns <= 64 / P)
@@ -908,12 +874,7 @@ int be_board_observe(be_board* b, const be_board_state* st, const be_board_out* 
   return board_launch(b, st, out, 2, nullptr, nullptr, nullptr, nullptr, 0, stream);
 }
 
-#ifdef BE_DIAG_STAMPS
-// diagnostics build only: the per-wave phase cycles of the last board launch (BDIAG_WAVES x 8)
-int be_board_diag_stamps(unsigned long long* cy) {
-  return hipMemcpyFromSymbol(cy, HIP_SYMBOL(g_bdiag), sizeof(g_bdiag)) == hipSuccess ? BE_OK : BE_E_HIP;
-}
-#endif
+BE_DIAG_BOARD_ENTRIES   // diagnostics builds only (diag.h)
 
 int be_board_status(be_board* b, int32_t* status_out, void* stream) {
   if (!b || !status_out) return bfail(b, BE_E_INVALID, "bad arguments to be_board_status");

@@ -40,9 +40,7 @@ struct BParams {
 // unrolled pass: every LDS read issued before the first store, write-through (sc1) buffer stores --
 // they drain while the wave runs instead of in the kernel-end L2 write-back -- and a descriptor of
 // N * 16 bytes that drops the last pass's extra lanes (no branch)
-#ifndef BE_BLOCKS_AUX
-#define BE_BLOCKS_AUX 16   // cache-policy bits of the copy-out (gfx950: sc1 16; A/B builds: 0 plain)
-#endif
+constexpr int BLOCKS_AUX = 16;   // cache-policy bits of the copy-out (gfx950: sc1 16)
 template <int N>
 __device__ __forceinline__ void copy_chunks(const uint8_t* stage, uint8_t* dst, int lane) {
   constexpr int IT = (N + 63) / 64;
@@ -55,7 +53,7 @@ __device__ __forceinline__ void copy_chunks(const uint8_t* stage, uint8_t* dst, 
                                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)du));
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dstu, (short)0, N * 16, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < IT; ++j) __builtin_amdgcn_raw_buffer_store_b128(x[j], rsrc, (lane + 64 * j) * 16, 0, BE_BLOCKS_AUX);
+  for (int j = 0; j < IT; ++j) __builtin_amdgcn_raw_buffer_store_b128(x[j], rsrc, (lane + 64 * j) * 16, 0, BLOCKS_AUX);
 }
 
 constexpr int BLK_ROW = 29, BLK_WAVE_U8 = 64 * BLK_ROW, BLK_WAVE_F32 = 64 * BLK_ROW * 4;
@@ -78,10 +76,7 @@ __global__ __launch_bounds__(256) void blocks_kernel(BParams p) {
   // obstacles in chunks of CH: every load of a chunk is issued before the first is used (clamped to
   // a real obstacle, the extra slots masked), so a wave waits for memory once per chunk instead of
   // once per pair of obstacles
-#ifndef BE_BLOCKS_CH
-#define BE_BLOCKS_CH 6    // obstacles per load chunk (18: slower at 65 536 envs, profiles/r03_blocks_ab.txt)
-#endif
-  constexpr int CH = BE_BLOCKS_CH;
+  constexpr int CH = 6;   // obstacles per load chunk (18: slower at 65 536 envs, profiles/r03_blocks_ab.txt)
   const int nobs = p.ns + p.nd;
   for (int k0 = 0; k0 < nobs; k0 += CH) {
     int32_t o[CH];

@@ -52,6 +52,14 @@ class _Draws:
         return int(self.rng.randint(lo, hi))
 
 
+class _Wrapped:
+    """gym's wrapper as prep_state4 sees it: ``env.unwrapped`` is the BallEnv."""
+    __slots__ = ("unwrapped",)
+
+    def __init__(self, env):
+        self.unwrapped = env
+
+
 class PyBallEnv:
     def __init__(self, **cfg):
         c = dict(DEFAULTS)
@@ -63,6 +71,7 @@ class PyBallEnv:
         self.total_distance = None
         self.total_reward_accumulated = 0.0
         self.elapsed = 0
+        self._env = _Wrapped(self)
 
     # ballenv_env.py:179-191
     @staticmethod
@@ -182,36 +191,47 @@ class PyBallEnv:
         reward, obs_flag = self._reward(dist)
         self.total_reward_accumulated += reward
         self.elapsed += 1
+        np.array(self.state, dtype=object)   # the reference returns np.array(self.state) (:289)
         return self.state, reward, goal_flag or obs_flag
 
-    def prep_state4(self, state, window):
-        """Quadrant one-hot ++ W*W occupancy window, as a list of 0/1 ints."""
-        out = [0] * (4 + window * window)
+    def prep_state2(self, state):
+        """Quadrant one-hot of the goal relative to the agent (ball_cnn_ac3.py:330-352)."""
+        q = np.zeros(4)
         ax, ay = state[0]
         gx, gy = state[1]
         dx, dy = gx - ax, gy - ay
         if dx >= 0 and dy >= 0:
-            out[1] = 1
+            q[1] = 1
         elif dx < 0 and dy >= 0:
-            out[0] = 1
+            q[0] = 1
         elif dx < 0 and dy < 0:
-            out[3] = 1
+            q[3] = 1
         else:
-            out[2] = 1
-        sx, sy = self.c["speed_x"], self.c["speed_y"]
-        start_x = ax - sx * int(window / 2)
-        start_y = ay - sy * int(window / 2)
-        cur_y = start_y
+            q[2] = 1
+        return q
+
+    def prep_state4(self, state, window):
+        """Quadrant one-hot ++ W*W occupancy window (f64 0/1 numpy row, as the reference builds
+        it before its torch conversion).  Like the reference it reaches the env's settings and
+        check_overlap through ``env.unwrapped`` inside the cell x obstacle loop."""
+        env = self._env
+        out = np.zeros(4 + window * window)
+        out[0:4] = self.prep_state2(state)
         counter = 4
+        ax, ay = state[0]
+        step_x, step_y = env.unwrapped.c["speed_x"], env.unwrapped.c["speed_y"]
+        start_x = ax - env.unwrapped.c["speed_x"] * int(window / 2)
+        start_y = ay - env.unwrapped.c["speed_y"] * int(window / 2)
+        cur_y = start_y
         for r in range(window):
             for cc in range(window):
-                cur_x = start_x + sx * cc
+                cur_x = start_x + step_x * cc
                 for i in range(3, len(state)):
-                    if self.check_overlap((cur_x, cur_y), state[i]):
+                    if env.unwrapped.check_overlap((cur_x, cur_y), state[i]):
                         out[counter] = 1
                         break
                 counter += 1
-            cur_y = start_y + sy * r
+            cur_y = start_y + step_y * r
         return out
 
 

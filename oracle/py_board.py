@@ -115,6 +115,7 @@ class PyBoard:
         self.state[2] = self.distance(self.state[0], self.state[1])
         reward, done = self.calc_reward()
         self.sensor_readings = features(self.state, self.obstacle_list, self.agent_vel, self.agent_radius)
+        np.array(self.state, dtype=object)        # the reference returns np.asarray(self.state) (:675)
         return self.state, reward, done
 
     def calc_reward(self):

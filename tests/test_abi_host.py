@@ -180,12 +180,12 @@ def test_python_port_matches_golden_subset():
         env = PyBallEnv()
         env.set_state(fx["init_agent"][e], fx["init_goal"][e], fx["init_prev_dist"][e], fx["init_total_dist"][e],
                       fx["init_static"][e], fx["init_dyn"][e], fx["init_dyn_goal"][e])
-        assert env.prep_state4(env.state, 10) == list(fx["init_obs10"][e])
+        assert np.array_equal(env.prep_state4(env.state, 10), fx["init_obs10"][e])
         for t in range(200):
             draws = [[int(v) for v in fx["tape"][e, t, k] if v >= 0] for k in range(5)]
             state, r, d = env.step(ML[fx["actions"][e, t]], draws_per_obstacle=draws)
             assert r == fx["reward"][e, t] and d == bool(fx["done"][e, t]), (e, t)
-            assert env.prep_state4(state, 5) == list(fx["obs5"][e, t]), (e, t)
+            assert np.array_equal(env.prep_state4(state, 5), fx["obs5"][e, t]), (e, t)
 
 
 def test_python_port_resets_match_golden():

@@ -23,6 +23,14 @@ def test_cpu_baseline_leg_small_sample():
     assert r["config1"]["env_steps_per_s"] > 0
 
 
+def test_board_cpu_baseline_leg_small_sample():
+    """The createBoard CPU baseline (oracle/py_board.py on the host cores) beside the board leg."""
+    import bench
+    r = bench.board_cpu_baseline(0.4, procs=2)
+    assert r["kind"] == "port" and r["unit"] == "env-steps/s" and r["cores"] == min(2, bench.host_cores())
+    assert r["env_steps"] > 0 and r["value"] > 0 and r["per_core_min"] <= r["per_core"] <= r["per_core_max"]
+
+
 @pytest.mark.gpu
 def test_bench_json_line(gpu):
     cmd = [sys.executable, "bench.py", "--steps", "20", "--warmup", "5", "--settle", "60", "--no-cpu-baseline",

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B library builds (git-ignored, under tools/diag/<name>/libballenv.so): the whole library from the
 # current sources through build.py (its per-unit flags included) with extra defines, e.g.
-#   bash tools/build_ab_lib.sh boardold -DBE_BOARD_NO_FAST_RESET
+#   bash tools/build_ab_lib.sh ct128 -DBE_S2_CT=128
 #   bash tools/build_ab_lib.sh st -DBE_DIAG_STAMPS
 set -eu
 cd "$(dirname "$0")/.."

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-3 GPU session: GPU tests, smoke, the driver-shaped and default bench lines, rocprofv3 kernel
+# A round GPU session (ROUND=r04 names the output dir): GPU tests, smoke, the driver-shaped and default bench lines, rocprofv3 kernel
 # stats (headline; config 2 + large batch; fused legs), PMC passes (config 2 / large batch / the
 # headline step kernel).  Every GPU step under its own time limit; a crash/timeout stops the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/r3c
+mkdir -p gpurun_out/${ROUND:-r04}_check
 export TMPDIR=/tmp
-O=gpurun_out/r3c
+O=gpurun_out/${ROUND:-r04}_check
 step() {  # name timeout cmd...
   local name=$1 t=$2; shift 2
   timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
@@ -35,10 +35,10 @@ if [ "${PROFILE:-1}" = "1" ]; then
   find $O/prof_fused -name "*kernel_stats.csv" -exec head -8 {} \;
 fi
 if [ "${PMC:-1}" = "1" ]; then
-  step pmc_c2_large 600 bash tools/pmc_passes.sh r3c/pmc --no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 \
+  step pmc_c2_large 600 bash tools/pmc_passes.sh ${ROUND:-r04}_check/pmc --no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 \
       --board-steps 0 --rollout-steps 0 --cold-steps 0 --from-reset-steps 0 --blocks-launches 0 --config2-steps 200 --large-steps 100
-  python tools/pmc_report.py $O/pmc "stepw_kernel<5, 13, 5, 8>" 4096 --out $O/r03_pmc_config2.json > /dev/null
-  python tools/pmc_report.py $O/pmc "be_kernel<10, 0, 13, 5>" 1048576 --out $O/r03_pmc_large_batch.json > /dev/null
+  python tools/pmc_report.py $O/pmc "stepw_kernel<5, 13, 5, 8>" 4096 --out $O/${ROUND:-r04}_pmc_config2.json > /dev/null
+  python tools/pmc_report.py $O/pmc "be_kernel<10, 0, 13, 5>" 1048576 --out $O/${ROUND:-r04}_pmc_large_batch.json > /dev/null
   step pmc_step 700 bash tools/pmc_bench.sh
   tail -1 $O/pmc_step.log
 fi

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-3 closing run: the full GPU suite and smoke, the driver's bench commands, and a rocprofv3
+# A round's closing run (ROUND=r04 names the output dir): the full GPU suite and smoke, the driver's bench commands, and a rocprofv3
 # kernel trace of the default bench command with its per-region summary (tools/trace_regions.py).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/r3final; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/${ROUND:-r04}_final; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -ne 0 ] && { grep -E "^E |FAIL" $O/pytest_gpu.log | head -20; exit $rc; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
