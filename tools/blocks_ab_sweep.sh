@@ -8,7 +8,7 @@ O=gpurun_out/${ROUND:-r04}_blocks; mkdir -p $O
 for v in ${VARIANTS:-base}; do
   lib=""; [ "$v" != base ] && lib=tools/diag/$v/libballenv.so
   BALLENV_LIB=$lib timeout -k 10 200 python -u tools/lane_sweep.py --window ${W:-10} --envs ${ENVS:-32768,65536} \
-      --lanes ${LANES:-2} --reps ${REPS:-2} > $O/sweep_$v.jsonl 2>&1 || exit $?
+      --lanes ${LANES:-2} --reps ${REPS:-2} ${SWEEP_ARGS:-} > $O/sweep_${TAG:-w${W:-10}}_$v.jsonl 2>&1 || exit $?
 done
 if [ "${BENCH:-0}" = "1" ]; then
   timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
