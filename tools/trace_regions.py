@@ -6,7 +6,8 @@
 bench.py's headline leg launches the step kernel `warmup` times eagerly, replays the captured graph
 for `untimed` steps (settle), then times `steps` launches: launches warmup+untimed+1 ..
 warmup+untimed+steps of the headline kernel are the timed region.  The config-2 and large-batch legs
-are the last 1000 / 200 launches of their kernels."""
+are the last 1000 / 200 launches of their kernels; config 4 at one rank (262 144 envs, the one-lane
+kernel) is the 1000 launches of that kernel before the large-batch leg's 2 x 200."""
 import argparse
 import csv
 import statistics
@@ -42,6 +43,11 @@ if head:
     print(f"{head}: {len(L)} launches in the whole command; the headline's timed region (launches "
           f"{lo + 1}..{lo + len(reg)}) averages {avg_us(reg):.3f} us per launch; "
           f"65536 x 390 B / that = {65536 * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
+c4 = find("be_kernel<10, 0, 13, 5>")
+if c4 and len(runs[c4]) >= 1400:
+    reg = runs[c4][-1400:-400]
+    print(f"{c4} (config 4 at one rank, 262144 envs): the 1000 launches before the large-batch leg average "
+          f"{avg_us(reg):.3f} us; 262144 x 390 B / that = {262144 * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
 for prefix, last, what in (("stepw_kernel<5, 13, 5, 8>", 1000, "config 2, 4096 envs, W=5"),
                            ("be_kernel<10, 0, 13, 5>", 200, "2^20 envs, large_batch"),
                            ("board_kernel<6, false, 1>", 1000, "createBoard step, 65536 envs"),
