@@ -1566,14 +1566,10 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t x) {   // OR with the other
   return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
 }
 
-// L = 4 (four lanes per env, 16 envs per wave) for the small per-GPU shards of a split batch
-// (BASELINE config 4: 32 768 envs per GPU at N = 8): one block of CT = 128 threads is 32 envs,
-// one stats slot, folded by wave 0 after a block barrier at the end (as stepw_kernel does).
-template <int WT, int NSC, int NDC, int L = 2, int CT = S2_CT>
-__global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
-  static_assert(L == 2 || L == 4, "two or four lanes per env");
-  static_assert(L == 2 || CT / L == 32, "four lanes: 32-env blocks (one stats slot)");
-  constexpr int EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
+template <int WT, int NSC, int NDC>
+__global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
+  constexpr int CT = S2_CT;
+  constexpr int L = 2, EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
   constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;   // obstacle slots per lane
   constexpr int KR = Geo<WT>::K, F = Geo<WT>::F, NW = Geo<WT>::NW;
   constexpr int NQ = F / 8, HQ = (NQ + 1) / 2;                     // uint2 words per row / per lane
@@ -1587,8 +1583,8 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
 
   DIAG(0);
   if (DBG(DBG_EXIT_ENTRY)) return;
-  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
-  const int blk0 = (int)blockIdx.x * EPB, i = blk0 + tid / L, e0 = blk0 + w * EPW;
+  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & 1;
+  const int blk0 = (int)blockIdx.x * EPB, i = blk0 + (tid >> 1), e0 = blk0 + w * EPW;
   uint8_t* stage_blk = smem + (size_t)(SS + SD + 1) * CT * 4;   // [EPB envs][F]
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
@@ -1629,7 +1625,7 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
   // the very end, and a dependent load there would lengthen exactly the waves that reset
   double* const slot = p.stats ? p.stats + (size_t)(e0 / 32) * 8 : nullptr;
   double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sp2 = sp0;
-  if (slot && lane == 0 && e0 < N && (L == 2 || w == 0)) {
+  if (slot && lane == 0 && e0 < N) {
     sp0 = reinterpret_cast<const double2*>(slot)[0];
     sp1 = reinterpret_cast<const double2*>(slot)[1];
     sp2 = reinterpret_cast<const double2*>(slot)[2];
@@ -1663,9 +1659,7 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
     const int k = L * j + h;
     const bool real = k < NDC;
     int ox = px(dp[j]), oy = py(dp[j]);
-    uint32_t f;
-    if constexpr (L == 2) f = h ? pick_field(b0, min(L * j + 1, 4)) : pick_field(b0, L * j);
-    else f = pick_field(b0, min(L * j + h, 4));
+    const uint32_t f = h ? pick_field(b0, min(L * j + 1, 4)) : pick_field(b0, L * j);
     uint32_t fl = 0u;
     ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[min(k, NDC - 1)], change, f, fl);
     st_flags |= real ? fl : 0u;
@@ -1704,8 +1698,8 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
   for (int j = 0; j < SD; ++j) obstacle_pk(dnew[j], L * j + h < NDC, hd);
 #pragma unroll
   for (int j = 0; j < SS; ++j) obstacle_pk(so[j], L * j + h < NSC, hs);
-  hs = group_or<L>((uint32_t)hs) != 0u;
-  hd = group_or<L>((uint32_t)hd) != 0u;
+  hs = pair_or((uint32_t)hs) != 0u;
+  hd = pair_or((uint32_t)hd) != 0u;
   DIAG(10);
 
   // ---- distance, reward, done (ballenv_env.py:268-286, 200-229), on both lanes
@@ -1718,7 +1712,7 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
   const bool trunc = p.time_limit > 0 && len >= p.time_limit;
   const bool done = env_done || trunc;
   const bool do_reset = valid && done && p.autoreset;
-  if (valid && L == 2) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
+  if (valid) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
     double* pd = h ? p.ep_return : p.reward;
     st_wt(pd + i, h ? ret : reward);
     int32_t* pi = h ? p.ep_len : p.agent;
@@ -1730,19 +1724,6 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
       if (!h && p.final_return) st_wt(p.final_return + i, ret);
       if (h && p.final_len) st_wt(p.final_len + i, len);
     }
-  } else if (valid) {   // four lanes: reward + done | ep_return + truncated | prev_dist + agent | ep_len
-    double* pd = h == 0 ? p.reward : (h == 1 ? p.ep_return : p.prev_dist);
-    if (h < 3) st_wt(pd + i, h == 0 ? reward : (h == 1 ? ret : dist));
-    if (h == 2) st_wt(p.agent + i, pk(ax, ay));
-    if (h == 3) st_wt(p.ep_len + i, len);
-    uint8_t* pb = h ? p.truncated : p.done;
-    if (pb && h < 2) st_wt(pb + i, (uint8_t)(h ? (trunc && !env_done) : done));
-    if (done) {
-      if (h == 1 && p.final_return) st_wt(p.final_return + i, ret);
-      if (h == 3 && p.final_len) st_wt(p.final_len + i, len);
-    }
-  }
-  if (valid) {
     // (stored after done is known: measured faster than storing inside the obstacle loop)
 #pragma unroll
     for (int j = 0; j < SD; ++j) {
@@ -1771,7 +1752,7 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
     uint32_t rows[KR], flat[NW];
     raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
 #pragma unroll
-    for (int k = 0; k < KR; ++k) rows[k] = group_or<L>(rows[k]);
+    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k]);
     flatten<WT>(rows, flat);
     if (!h) write_row_global<WT>(p.terminal_obs + (int64_t)i * F, flat, quadrant(ax, ay, gx, gy));
   }
@@ -1785,29 +1766,18 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
-      // every lane of the group takes the new agent / goal / rows; each scalar is stored by the
-      // lane that stored it in the physics above, so same-address stores stay in one lane's
-      // program order (two lanes: lane 1 ep_return / ep_len; four: lane 1 ep_return, lane 2
-      // agent / prev_dist, lane 3 ep_len)
+      // both lanes take the new agent / goal / rows; each scalar is stored by the lane that stored
+      // it in the physics above (lane 1: ep_return / ep_len), so same-address stores stay in one
+      // lane's program order
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
-      if constexpr (L == 2) {
-        if (h) {
-          st_wt(p.ep_return + i, 0.0);
-          st_wt(p.ep_len + i, 0);
-          return;
-        }
-        st_wt(p.agent + i, ag);
-        st_wt(p.prev_dist + i, prev);
-      } else {
-        if (h == 1) st_wt(p.ep_return + i, 0.0);
-        if (h == 3) st_wt(p.ep_len + i, 0);
-        if (h == 2) {
-          st_wt(p.agent + i, ag);
-          st_wt(p.prev_dist + i, prev);
-        }
-        if (h) return;
+      if (h) {
+        st_wt(p.ep_return + i, 0.0);
+        st_wt(p.ep_len + i, 0);
+        return;
       }
+      st_wt(p.agent + i, ag);
+      st_wt(p.prev_dist + i, prev);
       st_wt(p.goal + i, go);
       st_wt(p.total_dist + i, td);
       st_wt(p.episode + i, episode + 1u);
@@ -1828,25 +1798,9 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
     uint32_t rows[KR], flat[NW];
     raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
 #pragma unroll
-    for (int k = 0; k < KR; ++k) rows[k] = group_or<L>(rows[k] | xrows[k]);
+    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k] | xrows[k]);
     flatten<WT>(rows, flat);
     const int quad = quadrant(ax, ay, gx, gy);
-    if constexpr (L == 4) {
-      // lane h writes uint2 row words [q0, q0 + nq) = [0, 4) / [4, 7) / [7, 10) / [10, 13): word q
-      // holds cells 8q-4 .. 8q+3 (word 0 starts with the quadrant one-hot); c = the lane's cells
-      // from bit 0
-      const int q0 = h == 0 ? 0 : 3 * h + 1, nq = h == 0 ? 4 : 3;
-      const uint32_t c = h == 0 ? flat[0] << 4
-                       : h == 1 ? (flat[0] >> 28) | (flat[1] << 4)
-                       : h == 2 ? (flat[1] >> 20) | (flat[2] << 12) : (flat[2] >> 12) | (flat[3] << 20);
-      auto word4 = [&](int jj) -> uint32_t { return (((c >> (4 * jj)) & 0xFu) * 0x00204081u) & 0x01010101u; };
-      uint2* dst = reinterpret_cast<uint2*>(stage + (lane >> 2) * F) + q0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t w0 = (q == 0 && h == 0) ? 1u << (8 * quad) : word4(2 * q);
-        if (q < nq) dst[q] = make_uint2(w0, word4(2 * q + 1));
-      }
-    } else {
     // uint2 word q of this lane is row word 2(q + 7h) .. +1: word j >= 1 expands cells
     // 4(j-1) .. 4(j-1)+3.  c holds this lane's cells from bit 0: lane 0 cells -4.. (its word 0
     // is the quadrant one-hot), lane 1 cells 52..
@@ -1862,7 +1816,6 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
     for (int q = 0; q < HQ; ++q) {
       const uint32_t w0 = q == 0 ? (h ? word(0) : 1u << (8 * quad)) : word(2 * q);
       if (q < NQ - HQ || !h) dst[q] = make_uint2(w0, word(2 * q + 1));
-    }
     }
   }
   DIAG(4);
@@ -1881,26 +1834,7 @@ __global__ __launch_bounds__(CT, 2) void step2_kernel(KParams p) {
   // the episode statistics fold after the obs stores are issued: off the path to the last store
   // (6.55 -> 6.45 us; a reset leaves this lane's ret / len registers as the finished episode's)
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
-  if constexpr (L == 2) {
-    if (slot && !DBG(DBG_NO_STATS)) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
-  } else {   // the block's 32 envs span both waves: through LDS, one barrier, wave 0 folds in env order
-    __shared__ uint8_t s_fin[32];
-    __shared__ double s_fret[32];
-    __shared__ int s_flen[32];
-    if (slot && !DBG(DBG_NO_STATS)) {
-      const int el = tid / L;
-      if (h == 0) {
-        s_fin[el] = (done && valid) ? 1 : 0;
-        s_fret[el] = ret;
-        s_flen[el] = len;
-      }
-      __syncthreads();
-      if (w == 0) {
-        const bool d = lane < 32 && s_fin[lane & 31];
-        if (__ballot(d)) ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
-      }
-    }
-  }
+  if (slot && !DBG(DBG_NO_STATS)) ws = wave_stats(done && valid && h == 0, ret, len);   // even lanes: env order
   if (slot && lane == 0 && ws.n > 0.0) {
     reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
     reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
@@ -3013,17 +2947,6 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lane
   bool staged = true;
   const bool fixed = fixed_ok && mode == MODE_STEP && c.num_static == FIX_NS && c.num_dynamic == FIX_ND &&
                      c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
-  if (fixed && lanes10 == 4 && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
-    // four lanes per env: 16 envs per wave, 32 per 128-thread block
-    constexpr int CT4 = 128;
-    L.fn = step2_kernel<10, FIX_NS, FIX_ND, 4, CT4>;
-    L.epb = CT4 / 4;
-    L.threads = CT4;
-    constexpr int SLOTS = (FIX_NS + 3) / 4 + (FIX_ND + 3) / 4 + 1;
-    L.lds = SLOTS * CT4 * 4 + L.epb * F;
-    snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d, 4, %d>", FIX_NS, FIX_ND, CT4);
-    return L;
-  }
   if (fixed && lanes10 == 2 && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
     // two lanes per env (step2_kernel): 32 envs per wave, 128 per block
     L.fn = step2_kernel<10, FIX_NS, FIX_ND>;
@@ -3120,7 +3043,7 @@ struct be_ctx {
   bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
-  int step_lanes;      // W = 10: lanes per env of the fixed step kernel (1: be_kernel; 2 / 4: step2_kernel)
+  int step_lanes;      // W = 10: lanes per env of the fixed step kernel (1: be_kernel; 2: step2_kernel)
   int step5_lpe;       // W = 5: lanes per env of the fixed step kernel (1: be_kernel; 4 / 8: stepw_kernel)
   int roll5_lpe;       // W = 5: lanes per env of the fused rollout (1: rollout_kernel; 4 / 8: rolloutw_kernel)
   int max_lds;         // the device's LDS bytes per workgroup
@@ -3362,10 +3285,11 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
     else if (!strcmp(l, "4")) ctx->step5_lpe = 4;
     else if (!strcmp(l, "8")) ctx->step5_lpe = 8;
   }
-  if (const char* l = getenv("BALLENV_STEP_LPE")) {   // A/B override: exactly "1", "2" or "4", else ignored
+  // (four lanes per env, step2_kernel<10, 13, 5, 4, 128> of commit b0bc389, was bit-exact but slower
+  // at every size: 6.08 vs 5.28 us at 32 768 envs, profiles/r04_w10_lanes_2_4.jsonl)
+  if (const char* l = getenv("BALLENV_STEP_LPE")) {   // A/B override: exactly "1" or "2", else ignored
     if (!strcmp(l, "1")) ctx->step_lanes = 1;
     else if (!strcmp(l, "2")) ctx->step_lanes = 2;
-    else if (!strcmp(l, "4")) ctx->step_lanes = 4;
   }
   if (hipDeviceGetAttribute(&ctx->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess ||
       ctx->max_lds <= 0)
