@@ -106,8 +106,6 @@ struct KParams {
   int32_t prev_read;           // 1: read prev_dist; 0 (A/B only, when no reset can re-sample the agent,
                                // Q9): prev_dist == calc_dist(goal, agent), recomputed
   int32_t steps;               // rollout_kernel: steps per launch (actions / outputs are (steps, N, ...))
-  uint32_t* pcache;            // stepw_kernel: (N, 8) words per env, the next step's obstacle Philox block
-                               // + its (episode, ep_len) tag (context-owned; see stepw_kernel)
   // fused policy rollouts (rollout_kernel with HT > 0, be_policy_rollout)
   int32_t pol_bytes, pol_actions;
   const uint8_t* pol_img;      // packed Policy(W) image (policy_core.h PolLayout)
@@ -1862,16 +1860,6 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
 //  * the block's 32 envs share one stats slot: every wave leaves its finished envs' return and
 //    length in LDS after the physics, and after a block barrier wave 0 folds them in env order --
 //    the same sums, in the same order, as the one-lane kernel.
-// XCD-aware block order (cdna_hip_programming.md T1): blocks b and b + 8 are observed to share an
-// XCD (round-robin dealing), so the blocks of one XCD take consecutive env ranges.  A 32-env
-// block's byte-array spans (action, dyn_goal, done, truncated: 32 B each) then share their 128-B
-// lines within one XCD's L2 instead of each line being fetched by up to four XCDs.  Bijective for
-// any grid size; a speed choice only (placement is not part of HIP's contract).
-__device__ __forceinline__ int xcd_block(int b, int nwg) {
-  const int q = nwg / 8, r = nwg % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
 template <int L>
 __device__ __forceinline__ uint32_t lane_group_or(uint32_t x) {   // OR over the aligned group of L lanes
   static_assert(L == 4 || L == 8, "L must be 4 or 8");
@@ -1903,8 +1891,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   if (DBG(DBG_EXIT_ENTRY)) return;
   PH_INIT;
   const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
-  const int bid = xcd_block((int)blockIdx.x, (int)gridDim.x);
-  const int el = tid / L, blk0 = bid * 32, i = blk0 + el, e0 = blk0 + w * EPW;
+  const int el = tid / L, blk0 = (int)blockIdx.x * 32, i = blk0 + el, e0 = blk0 + w * EPW;
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
   uint8_t* stage = &s_stage[w][0];
@@ -1917,9 +1904,6 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid + j * CT, TW - 1));
   const uint32_t episode = ld_s(p.episode, ic);
   const int len0 = ld_s(p.ep_len, ic);
-  // this step's obstacle Philox block as the previous step computed it, with its tag
-  const uint4 pc = ld_s(reinterpret_cast<const uint4*>(p.pcache), 2u * ic);
-  const uint2 ptag = ld_s(reinterpret_cast<const uint2*>(p.pcache), 4u * ic + 2u);
   const int32_t agent0 = ld_s(p.agent, ic), goal0 = ld_s(p.goal, ic);
   int32_t dp[SD], so[SS];
   int dgi[SD];
@@ -1946,7 +1930,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const int a = ld_s(p.actions, ic);
   __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any of them is used
   const double old_dist = p.prev_read ? old_read : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
-  double* const slot = p.stats ? p.stats + (size_t)bid * 8 : nullptr;
+  double* const slot = p.stats ? p.stats + (size_t)blockIdx.x * 8 : nullptr;
   double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sp2 = sp0;
   if (slot && tid == 0) {   // the block's stats slot, read now (wave 0 folds into it)
     sp0 = reinterpret_cast<const double2*>(slot)[0];
@@ -1969,18 +1953,7 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   if (counter < 0) counter += p.goal_change + 1;
   if (counter > p.goal_change) counter -= p.goal_change + 1;
   const bool change = counter >= p.goal_change;
-  // The obstacle draws' Philox block is a pure function of (env id, episode, ep_len, seed), so the
-  // previous launch computed this step's block ahead, off its dependent chain, and left it in the
-  // context's cache tagged with the (episode, ep_len) it is for.  A tag that does not match (the
-  // first step, a reset, an outside edit of the state) falls back to computing it here: the
-  // draws are the same either way, bit for bit.
-  u4 b0{pc.x, pc.y, pc.z, pc.w};
-  const bool cached = ptag.x == episode && ptag.y == (uint32_t)len0;
-  if (__ballot(!cached)) {
-    const u4 bc = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
-    if (!cached) b0 = bc;
-  }
-  if (DBG(DBG_NO_PHILOX)) b0 = u4{gid, episode, 7u, 9u};
+  const u4 b0 = DBG(DBG_NO_PHILOX) ? u4{gid, episode, 7u, 9u} : philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
   uint32_t st_flags = 0u;
   int ngs[SD];
   int32_t dnew[SD];
@@ -1994,9 +1967,6 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     dnew[j] = pk(ox, oy);
   }
   PH(1);
-  // the next step's block (this episode, ep_len + 1: a reset makes it stale, and its tag says so),
-  // computed where it can fill the latency of this step's chain
-  const u4 bn = philox(gid, episode, (uint32_t)len0 + 1u, tag(PURPOSE_STEP_OBS, 0u), p.seed);
   // ---- action -> agent move + clamp (ballenv_env.py:247-259); unit moves and speeds
   st_flags |= a >= p.num_actions ? (uint32_t)BE_STATUS_BAD_ACTION : 0u;
   const uint32_t sh = 2u * (uint32_t)(a < p.num_actions ? a : 0);
@@ -2055,9 +2025,6 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
       if (h == 2 && p.final_return) st_wt(p.final_return + i, ret);
       if (h == 3 && p.final_len) st_wt(p.final_len + i, len);
     }
-    // the next step's Philox block and its tag, from lanes with few stores of their own
-    if (h == L / 2) reinterpret_cast<uint4*>(p.pcache)[2 * i] = make_uint4(bn.x, bn.y, bn.z, bn.w);
-    if (h == L / 2 + 1) reinterpret_cast<uint2*>(p.pcache)[4 * i + 2] = make_uint2(episode, (uint32_t)len);
 #pragma unroll
     for (int j = 0; j < SD; ++j) {
       const int k = L * j + h;
@@ -2209,8 +2176,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
   constexpr int TW = (int)(sizeof(Tables) / 4);
 
   const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63, h = lane & (L - 1);
-  const int bid = xcd_block((int)blockIdx.x, (int)gridDim.x);
-  const int el = tid / L, blk0 = bid * 32, i = blk0 + el, e0 = blk0 + w * EPW;
+  const int el = tid / L, blk0 = (int)blockIdx.x * 32, i = blk0 + el, e0 = blk0 + w * EPW;
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
   uint8_t* stage = &s_stage[w][0];
@@ -2237,7 +2203,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
 #pragma unroll
   for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
   double old_dist = ld_s(p.prev_dist, ic), total = ld_s(p.total_dist, ic), ret = ld_s(p.ep_return, ic);
-  double* const slot = p.stats ? p.stats + (size_t)bid * 8 : nullptr;   // one per 32 envs
+  double* const slot = p.stats ? p.stats + (size_t)blockIdx.x * 8 : nullptr;   // one per 32 envs
   WaveStats acc{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY};
   if (slot && tid == 0) acc = WaveStats{slot[0], slot[1], slot[2], slot[3], slot[4], slot[5]};
 #pragma unroll
@@ -2645,16 +2611,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
             Bt[ks] = v;
           }
         };
-        auto put = [&](int tt, const float (&part)[POL_OUT]) {   // lane group g4: outputs 4 g4 .. 4 g4 + 3
+        auto put = [&](int tt, const float (&part)[PolQ<NO>::N]) {   // lane group g4: outputs g4, g4 + 4, ...
 #pragma unroll
-          for (int q = 0; q < POL_OUT; ++q)
-            if (4 * g4 + q < NO) pbuf[((w * NWAVE + tt) * 16 + (lane & 15)) * NO + 4 * g4 + q] = part[q];
+          for (int q = 0; q < PolQ<NO>::N; ++q)
+            if (4 * q + g4 < NO) pbuf[((w * NWAVE + tt) * 16 + (lane & 15)) * NO + 4 * q + g4] = part[q];
         };
         constexpr int HTC = HT > 0 ? HT : 1;
         const int h0 = pol_chunk_begin(HTC, w), h1 = pol_chunk_begin(HTC, w + 1);
         for (int tt = 0; tt < nt; tt += 2) {   // two tiles at a time: shared weight reads, interleaved chains
           v4i Ba[KS], Bb[KS];
-          float pa[POL_OUT], pb[POL_OUT];
+          float pa[PolQ<NO>::N], pb[PolQ<NO>::N];
           load_b(tt, Ba);
           if (tt + 1 < nt && !DBG(0xF0000u)) {
             load_b(tt + 1, Bb);
@@ -3039,7 +3005,6 @@ struct be_ctx {
   int device;
   int* status;
   Tables* d_tables;
-  uint32_t* pcache;    // stepw_kernel's Philox-ahead cache: (N, 8) words, allocated when it can run
   bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
@@ -3322,17 +3287,11 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   if (e == hipSuccess) e = hipMemset(ctx->status, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&ctx->d_tables, sizeof(Tables));
   if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, &ctx->tables, sizeof(Tables), hipMemcpyHostToDevice);
-  if (e == hipSuccess && cfg->window == 5 && ctx->step5_lpe != 1) {   // stepw_kernel may run: its cache, tags invalid
-    const size_t pb = (size_t)cfg->num_envs * 32;
-    e = hipMalloc(&ctx->pcache, pb);
-    if (e == hipSuccess) e = hipMemset(ctx->pcache, 0xFF, pb);
-  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     int rc = fail(nullptr, BE_E_HIP, "HIP error in be_create: %s", hipGetErrorString(e));
     if (ctx->status) (void)hipFree(ctx->status);
     if (ctx->d_tables) (void)hipFree(ctx->d_tables);
-    if (ctx->pcache) (void)hipFree(ctx->pcache);
     delete ctx;
     return rc;
   }
@@ -3344,7 +3303,6 @@ int be_destroy(be_ctx* ctx) {
   if (!ctx) return BE_OK;
   if (ctx->status) (void)hipFree(ctx->status);
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
-  if (ctx->pcache) (void)hipFree(ctx->pcache);
   delete ctx;
   return BE_OK;
 }
@@ -3371,7 +3329,6 @@ static KParams make_params(be_ctx* ctx, const be_state* st, const be_out* out) {
     a.final_len = out->final_len; a.stats = out->stats;
   }
   a.tables = ctx->d_tables;
-  a.pcache = ctx->pcache;
   a.status = ctx->status;
   return a;
 }

@@ -89,21 +89,6 @@ __device__ __forceinline__ void bst(T* p, T v) {
   if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
-// An (x, y) f64 pair of env i (agent, goal: (N, 2) arrays) as ONE 16-byte store: a wave's pairs are
-// whole 128-B lines, where two 8-byte stores at a 16-byte stride each write half of every line --
-// partial-line writes at the memory side once they are write-through (sc1: buffer-store aux bit).
-template <bool WT>
-__device__ __forceinline__ void bst2(double* base, int i, double x, double y) {
-  if constexpr (WT) {
-    typedef int v4i_ __attribute__((ext_vector_type(4)));
-    const unsigned long long bx = (unsigned long long)__double_as_longlong(x), by = (unsigned long long)__double_as_longlong(y);
-    const v4i_ v = {(int)(uint32_t)bx, (int)(uint32_t)(bx >> 32), (int)(uint32_t)by, (int)(uint32_t)(by >> 32)};
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, i * 16, 0, 16);   // aux 16 = sc1
-  } else {
-    reinterpret_cast<double2*>(base)[i] = make_double2(x, y);
-  }
-}
 __device__ __forceinline__ int sx(int32_t p) { return (int)(int16_t)(p & 0xFFFF); }
 __device__ __forceinline__ int sy(int32_t p) { return p >> 16; }
 
@@ -710,12 +695,14 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
 #pragma unroll
     for (int k = 0; k < MAXS; ++k)
       if (k < p.ns) bst<WT>(p.statics + (int64_t)k * p.n + i, so[k]);
-    bst2<WT>(p.goal, i, gx, gy);
+    bst<WT>(p.goal + 2 * (int64_t)i, gx);
+    bst<WT>(p.goal + 2 * (int64_t)i + 1, gy);
     bst<WT>(p.total + i, total);
     bst<WT>(p.episode + i, episode);
   }
   if (h == 0) {
-    bst2<WT>(p.agent, i, ax, ay);
+    bst<WT>(p.agent + 2 * (int64_t)i, ax);
+    bst<WT>(p.agent + 2 * (int64_t)i + 1, ay);
     bst<WT>(p.dist + i, dist);
   }
   if (h == L - 1) {
@@ -770,8 +757,6 @@ int be_board_create(const be_board_config* cfg, int32_t device, be_board** out) 
   if (!cfg || !out) return bfail(nullptr, BE_E_INVALID, "bad arguments to be_board_create");
   *out = nullptr;
   if (cfg->num_envs < 1) return bfail(nullptr, BE_E_INVALID, "num_envs must be >= 1");
-  if (cfg->num_envs > (1 << 26))   // the (N, 2) f64 pairs are addressed by 32-bit byte offsets (bst2)
-    return bfail(nullptr, BE_E_INVALID, "num_envs must be <= 2^26");
   if (cfg->num_static < 0 || cfg->num_static > BE_BOARD_MAX_STATIC)
     return bfail(nullptr, BE_E_INVALID, "num_static must be in [0, 32]");
   if (cfg->num_actions < 1 || cfg->num_actions > BE_BOARD_MAX_ACTIONS)

@@ -205,12 +205,12 @@ __global__ __launch_bounds__(POL_THREADS) void policy_kernel(PParams p) {
     v4i Bt[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) Bt[ks] = load_obs16<ALIGNED8>(p, e >= 0 ? blk0 + e : p.n, 64 * ks + 16 * g);
-    float out[POL_OUT];
+    float out[PolQ<NO>::N];
     tile_forward<HT, KS, NO>(lds, Bt, lane, p.dbg, out);
-    if (e >= 0) {   // lane group g holds outputs 4g .. 4g + 3
+    if (e >= 0) {   // lane group g holds outputs g, g + 4, ...
 #pragma unroll
-      for (int i = 0; i < POL_OUT; ++i)
-        if (4 * g + i < NO) lg[e * NO + 4 * g + i] = out[i];
+      for (int q = 0; q < PolQ<NO>::N; ++q)
+        if (4 * q + g < NO) lg[e * NO + 4 * q + g] = out[q];
     }
   }
   __syncthreads();

@@ -42,32 +42,30 @@ __host__ __device__ constexpr PolLayout pol_layout(int HT, int KS, int NO) {
 }
 
 
-// A tile's outputs in the layout of a v_mfma_f32_16x16x4f32 result: register i of lane group
-// g = lane >> 4 holds output 4g + i (NO <= 16; rows past NO are zero) of the env of column lane & 15.
-typedef float v4f __attribute__((ext_vector_type(4)));
-constexpr int POL_OUT = 4;
+// Sum over the 4 lane groups (lanes l, l^16, l^32, l^48) of four values at once: lane group
+// (row) r gets the full sum of value r, added as ((g0 + g1) + (g2 + g3)) -- two permlane16
+// swaps pair the values' rows, one permlane32 swap finishes all four (6 VALU instructions
+// where one value at a time takes 16).
+__device__ __forceinline__ float sum_groups4(float x0, float x1, float x2, float x3) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
+  const float c = __uint_as_float(a[0]) + __uint_as_float(a[1]);   // rows: x0 01, x1 01, x0 23, x1 23
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x2), __float_as_uint(x3), false, false);
+  const float e = __uint_as_float(b[0]) + __uint_as_float(b[1]);   // rows: x2 01, x3 01, x2 23, x3 23
+  const auto d = __builtin_amdgcn_permlane32_swap(__float_as_uint(c), __float_as_uint(e), false, false);
+  return __uint_as_float(d[0]) + __uint_as_float(d[1]);
+}
 
-// The heads of hidden row tile ht on the matrix cores: logits (16 outputs x 16 envs) +=
-// W'(outputs x 16 hidden) * relu(h)(16 hidden x 16 envs), as four K = 4 steps of
-// v_mfma_f32_16x16x4f32.  Step r takes hidden units 16 ht + 4 k + r (k = the lane group), so its
-// B operand is this lane's h[r] as it stands and its A operand is component r of the packed head
-// float4 of (row tile, lane group, output lane & 15): one LDS read per row, no VALU FMAs and no
-// cross-lane sums (the MFMA adds over the lane groups).
-template <int HT, int KS, int NO>
-__device__ __forceinline__ float4 head_weights(const uint8_t* lds, int ht, int lane) {
-  static_assert(NO <= 16, "one 16-row MFMA tile of outputs");
-  constexpr PolLayout L = pol_layout(HT, KS, NO);
-  const int g = lane >> 4, o = lane & 15;
-  const float4 w = *(const float4*)(lds + L.head + (((ht * 4 + g) * NO + (o < NO ? o : NO - 1)) * 4) * 4);
-  return o < NO ? w : make_float4(0.f, 0.f, 0.f, 0.f);
+// A tile's NO outputs in NQ = ceil(NO/4) registers: register q of lane group g holds output 4q + g.
+template <int NO> struct PolQ { static constexpr int N = (NO + 3) / 4; };
+template <int NO>
+__device__ __forceinline__ void sum_outputs(const float (&part)[NO], float (&out)[PolQ<NO>::N]) {
+#pragma unroll
+  for (int q = 0; q < PolQ<NO>::N; ++q) {
+    auto at = [&](int o) { return o < NO ? part[o] : 0.f; };
+    out[q] = sum_groups4(at(4 * q), at(4 * q + 1), at(4 * q + 2), at(4 * q + 3));
+  }
 }
-__device__ __forceinline__ v4f head_mfma(const float4& w, const float (&h)[4], v4f acc) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, h[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, h[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, h[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, h[3], acc, 0, 0, 0);
-  return acc;
-}
+
 
 // OR of x over lanes l, l^16, l^32, l^48
 // The packed image (global, 16-B words) into LDS by NT threads, U loads in flight per thread: a
@@ -105,22 +103,24 @@ __device__ __forceinline__ int digits(int hi, int mid, int lo) {
 }
 
 // Hidden rows are summed in 4 fixed chunks of 16-row tiles, chunk c = [c*HT/4, (c+1)*HT/4):
-// logit = ((s_0 + s_1) + s_2) + s_3 with s_c the chunk's chain of head MFMAs.
+// logit = ((s_0 + s_1) + s_2) + s_3 with s_c the chunk's FMA chain summed over the lane groups.
 // One wave can run all four (tile_forward) or four waves one each (the fused rollout kernel),
 // with the same result bit for bit.
 constexpr int POL_CHUNKS = 4;
 __host__ __device__ constexpr int pol_chunk_begin(int HT, int c) { return (c * HT) / POL_CHUNKS; }
 
 // One chunk [ht0, ht1) of the dense forward of a 16-env column tile (env of lane = lane & 15,
-// obs fragments B): fc1 on the int8 MFMA, relu, the heads on the f32 MFMA.  Returns the chunk's raw
-// logit partials (no head bias) in the POL_OUT layout: register i of lane group g holds output
-// 4g + i of the env of column lane & 15.
+// obs fragments B): fc1 on the int8 MFMA, relu, heads.  Returns the chunk's raw logit partials
+// (no head bias), summed over the lane groups, in PolQ layout: register q of lane group g holds
+// output 4q + g of the env of column lane & 15.
 template <int HT, int KS, int NO, int LEN = 0>
 __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS], int lane, int dbg, int ht0,
-                                           int ht1, float (&out)[POL_OUT]) {
+                                           int ht1, float (&out)[PolQ<NO>::N]) {
   constexpr PolLayout L = pol_layout(HT, KS, NO);
   const int g = lane >> 4;
-  v4f part = {0.f, 0.f, 0.f, 0.f};
+  float part[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) part[o] = 0.f;
   const int n = LEN > 0 ? LEN : ht1 - ht0;
 #pragma unroll
   for (int j = 0; j < (LEN > 0 ? LEN : HT); ++j) {
@@ -130,7 +130,6 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
     acc[0] = v4i{0, 0, 0, 0};
     acc[1] = v4i{0, 0, 0, 0};
     acc[2] = *(const v4i*)(lds + L.bias + (ht * 16 + 4 * g) * 4);
-    const float4 w = head_weights<HT, KS, NO>(lds, ht, lane);
     if (!(dbg & 2)) {
 #pragma unroll
       for (int d = 0; d < 3; ++d)
@@ -148,11 +147,17 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
       const int q = digits(acc[0][r], acc[1][r], acc[2][r]);
       h[r] = (float)(q > 0 ? q : 0);
     }
-    if (!(dbg & 4)) part = head_mfma(w, h, part);
-    else part[0] += h[0] + h[1] + h[2] + h[3];
-  }
+    if (!(dbg & 4)) {
 #pragma unroll
-  for (int i = 0; i < POL_OUT; ++i) out[i] = part[i];
+      for (int o = 0; o < NO; ++o) {
+        const float4 w = *(const float4*)(lds + L.head + (((ht * 4 + g) * NO + o) * 4) * 4);
+        part[o] = fmaf(w.w, h[3], fmaf(w.z, h[2], fmaf(w.y, h[1], fmaf(w.x, h[0], part[o]))));
+      }
+    } else {
+      part[0] += h[0] + h[1] + h[2] + h[3];
+    }
+  }
+  sum_outputs<NO>(part, out);
 }
 
 // tile_chunk for two tiles at once (B0, B1): the fc1 digit fragments and head weights are
@@ -162,10 +167,13 @@ __device__ __forceinline__ void tile_chunk(const uint8_t* lds, const v4i (&B)[KS
 // under row j's MFMAs); LEN == 0: a runtime trip count.
 template <int HT, int KS, int NO, int LEN = 0>
 __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[KS], const v4i (&B1)[KS], int lane,
-                                            int ht0, int ht1, float (&out0)[POL_OUT], float (&out1)[POL_OUT]) {
+                                            int ht0, int ht1, float (&out0)[PolQ<NO>::N],
+                                            float (&out1)[PolQ<NO>::N]) {
   constexpr PolLayout L = pol_layout(HT, KS, NO);
   const int g = lane >> 4;
-  v4f p0 = {0.f, 0.f, 0.f, 0.f}, p1 = p0;
+  float p0[NO], p1[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) { p0[o] = 0.f; p1[o] = 0.f; }
   const int n = LEN > 0 ? LEN : ht1 - ht0;
 #pragma unroll
   for (int j = 0; j < (LEN > 0 ? LEN : HT); ++j) {
@@ -176,7 +184,6 @@ __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[
     a0[1] = v4i{0, 0, 0, 0};
     a0[2] = *(const v4i*)(lds + L.bias + (ht * 16 + 4 * g) * 4);
     a1[0] = a0[0]; a1[1] = a0[1]; a1[2] = a0[2];
-    const float4 w = head_weights<HT, KS, NO>(lds, ht, lane);
 #pragma unroll
     for (int d = 0; d < 3; ++d)
 #pragma unroll
@@ -193,23 +200,27 @@ __device__ __forceinline__ void tile_chunk2(const uint8_t* lds, const v4i (&B0)[
       h0[r] = (float)(q0 > 0 ? q0 : 0);
       h1[r] = (float)(q1 > 0 ? q1 : 0);
     }
-    p0 = head_mfma(w, h0, p0);
-    p1 = head_mfma(w, h1, p1);
-  }
 #pragma unroll
-  for (int i = 0; i < POL_OUT; ++i) { out0[i] = p0[i]; out1[i] = p1[i]; }
+    for (int o = 0; o < NO; ++o) {
+      const float4 w = *(const float4*)(lds + L.head + (((ht * 4 + g) * NO + o) * 4) * 4);
+      p0[o] = fmaf(w.w, h0[3], fmaf(w.z, h0[2], fmaf(w.y, h0[1], fmaf(w.x, h0[0], p0[o]))));
+      p1[o] = fmaf(w.w, h1[3], fmaf(w.z, h1[2], fmaf(w.y, h1[1], fmaf(w.x, h1[0], p1[o]))));
+    }
+  }
+  sum_outputs<NO>(p0, out0);
+  sum_outputs<NO>(p1, out1);
 }
 
 // The whole dense forward of one tile on one wave: the four chunks in order.
 template <int HT, int KS, int NO>
 __device__ __forceinline__ void tile_forward(const uint8_t* lds, const v4i (&B)[KS], int lane, int dbg,
-                                             float (&out)[POL_OUT]) {
+                                             float (&out)[PolQ<NO>::N]) {
 #pragma unroll
   for (int c = 0; c < POL_CHUNKS; ++c) {
-    float part[POL_OUT];
+    float part[PolQ<NO>::N];
     tile_chunk<HT, KS, NO>(lds, B, lane, dbg, pol_chunk_begin(HT, c), pol_chunk_begin(HT, c + 1), part);   // (inlined: constant bounds)
 #pragma unroll
-    for (int i = 0; i < POL_OUT; ++i) out[i] = c == 0 ? part[i] : out[i] + part[i];
+    for (int q = 0; q < PolQ<NO>::N; ++q) out[q] = c == 0 ? part[q] : out[q] + part[q];
   }
 }
 
