@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/c2_ab; mkdir -p $O
 ARGS="--no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 --torch-policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 1000 --large-steps 0 --from-reset-steps 0 --blocks-launches 0"
-for r in 1 2; do
+for r in $(seq 1 ${REPS:-2}); do
   for v in new ${B:-stepwold}; do
     if [ $v = new ]; then L=""; else L=tools/diag/$v/libballenv.so; fi
     BALLENV_LIB=$L timeout -k 10 200 python3 bench.py $ARGS > $O/$v.$r.log 2>&1
