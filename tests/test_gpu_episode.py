@@ -120,6 +120,53 @@ def test_step_kernel_default_episode(gpu, W, N, a):
     env.close()
 
 
+@pytest.mark.parametrize("W", [10, 5])
+def test_step_kernel_top_of_id_space(gpu, W):
+    """A maximum-size case: 2^22 envs whose global ids end at the top of the 32-bit id space
+    (env_offset = 2^32 - 2^22, be_config_check's limit), the one-lane fixed-shape kernel; the
+    last 2048 envs (ids 2^32 - 2048 .. 2^32 - 1) bit-exact against the oracle over 40
+    default-config steps from random ep_len phases, truncations and goal changes included --
+    the Philox keys' 32-bit id arithmetic and index arithmetic past 2^24 envs."""
+    from gym_ballenv_amd.config import EnvConfig
+    from test_gpu_parity import KEYS as SK
+    cfg_py = EnvConfig()
+    N = 1 << 22
+    off, k = (1 << 32) - N, SLICE
+    a = N - k
+    env = make_env(cfg_py, N, W, gpu, seed=0xBA11, env_offset=off, terminal_obs=True)
+    assert env.kernel_name("step") == fixed_step_kernel(W, N) == f"be_kernel<{W}, 0, 13, 5>"
+    cfg = cfg_py.to_abi(k, W, env_offset=off + a, seed=0xBA11)
+    st = oracle.new_state(cfg)
+    out = oracle.new_out(cfg, terminal=True)
+    oracle.reset(cfg, st, out)
+    env.reset()
+    lens = _random_lens(N, np.random.default_rng(W))
+    env.ep_len.copy_(torch.from_numpy(lens).to(gpu))
+    st["ep_len"][:] = lens[a:]
+
+    def check_slice(msg):   # the slice only: the whole 2^22-env state is ~0.5 GB
+        for key in SK:
+            v = getattr(env, key)
+            got = (v[:, a:] if key in ("static_obs", "dyn_obs", "dyn_goal") else v[a:]).cpu().numpy()
+            want = st[key].view(np.int32) if key == "episode" else st[key]
+            np.testing.assert_array_equal(got, want, err_msg=f"{msg}: state[{key}]")
+
+    check_slice("after reset")
+    acts = env.sample_actions(40, seed=0xBA11)
+    n_trunc = 0
+    for t in range(40):
+        out["terminal_obs"][:] = 0
+        env.terminal_obs.zero_()
+        oracle.step(cfg, st, out, actions=acts[t, a:].cpu().numpy())
+        obs, reward, done, info = env.step(acts[t])
+        n_trunc += _check_step(t, a, k, out, obs, reward, done, info["truncated"], info["final_return"],
+                               info["final_len"], info["terminal_obs"])
+        check_slice(f"t={t}")
+    assert n_trunc > 0
+    env.status()
+    env.close()
+
+
 def test_step_kernel_time_limit_boundary(gpu):
     """Every env starts at ep_len 995..999: the TimeLimit truncates the survivors within five
     steps and the autoreset starts their next episode (ep_len 999 -> done, ep_len 0)."""
