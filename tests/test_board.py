@@ -294,3 +294,46 @@ def test_gpu_board_two_lanes_equal_one_lane(gpu, ns, monkeypatch):
     for b in boards:
         b.status()
         b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_board_top_of_id_space(gpu):
+    """createBoard at the top of the 32-bit global-id space (be_board_create's limit): 2^21 envs whose
+    ids end at 2^32 - 1.  The last 2048 envs' Philox reset and 40 steps of float moves with autoreset
+    (hits and goals; the oracle has no TimeLimit) are bit-exact against the oracle on the same global ids: state, rewards, dones,
+    and the features (f[18] to the usual rtol)."""
+    N, ns, k = 1 << 21, 6, 2048
+    off, a = (1 << 32) - N, N - k
+    b = make_board(gpu, N, ns, seed=0x70B, env_offset=off, autoreset=True)
+    cfg = type(b.cfg).from_buffer_copy(b.cfg)
+    cfg.num_envs, cfg.env_offset = k, off + a
+    st = oracle.board_new_state(cfg)
+
+    def check(msg):
+        for key in b.STATE_KEYS:
+            v = getattr(b, key)
+            got = (v[:, a:] if key == "static_obs" else v[a:]).cpu().numpy()
+            want = st[key].view(np.int32) if key == "episode" else st[key]
+            np.testing.assert_array_equal(got, want, err_msg=f"{msg}: {key}")
+
+    f = b.reset()
+    s, wf = oracle.board_reset_philox(cfg, st)
+    assert s == 0
+    check("reset")
+    check_features(f[a:].cpu().numpy(), wf, "reset")
+    g = torch.Generator(device=gpu).manual_seed(5)
+    n_done = 0
+    for t in range(40):
+        dl = torch.randn(N, 2, generator=g, dtype=torch.float64, device=gpu) * 4
+        f, r, d, _ = b.step(deltas=dl)
+        wr, wd, wf = oracle.board_step(cfg, st, deltas=dl[a:].cpu().numpy())
+        dm = wd.astype(bool)
+        _, wfr = oracle.board_reset_philox(cfg, st, mask=dm)
+        np.testing.assert_array_equal(r[a:].cpu().numpy(), wr, err_msg=f"reward t={t}")
+        np.testing.assert_array_equal(d[a:].cpu().numpy(), dm, err_msg=f"done t={t}")
+        check(f"t={t}")
+        check_features(f[a:].cpu().numpy(), np.where(dm[:, None], wfr, wf), f"t={t}")
+        n_done += int(dm.sum())
+    assert n_done > k // 50, n_done
+    b.status()
+    b.close()

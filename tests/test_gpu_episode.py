@@ -167,6 +167,47 @@ def test_step_kernel_top_of_id_space(gpu, W):
     env.close()
 
 
+def test_rollout_kernel_top_of_id_space(gpu):
+    """be_rollout (the fused random-action rollout, one-lane rollout_kernel) at the top of the 32-bit
+    global-id space: 2^21 envs ending at id 2^32 - 1, two launches of 20 steps; the last 2048 envs'
+    per-step outputs and state bit-exact against the oracle, truncations and goal changes included."""
+    from gym_ballenv_amd.config import EnvConfig
+    from test_gpu_parity import KEYS as SK
+    cfg_py = EnvConfig()
+    N, W = 1 << 21, 10
+    off, k = (1 << 32) - N, SLICE
+    a = N - k
+    env = make_env(cfg_py, N, W, gpu, seed=0x5EED, env_offset=off, terminal_obs=True)
+    assert env.kernel_name("rollout") == "rollout_kernel<10, 13, 5, 0, 1, 10>"
+    cfg = cfg_py.to_abi(k, W, env_offset=off + a, seed=0x5EED)
+    st = oracle.new_state(cfg)
+    out = oracle.new_out(cfg, terminal=True)
+    oracle.reset(cfg, st, out)
+    env.reset()
+    lens = _random_lens(N, np.random.default_rng(21))
+    env.ep_len.copy_(torch.from_numpy(lens).to(gpu))
+    st["ep_len"][:] = lens[a:]
+    acts = env.sample_actions(40, seed=23)
+    n_trunc, t0 = 0, 0
+    for K in (20, 20):
+        obs, reward, done, info = env.rollout(acts[t0:t0 + K])
+        for j in range(K):
+            t = t0 + j
+            out["terminal_obs"][:] = 0
+            oracle.step(cfg, st, out, actions=acts[t, a:].cpu().numpy())
+            n_trunc += _check_step(t, a, k, out, obs[j], reward[j], done[j], info["truncated"][j],
+                                   info["final_return"][j], info["final_len"][j], info["terminal_obs"][j])
+        t0 += K
+        for key in SK:
+            v = getattr(env, key)
+            got = (v[:, a:] if key in ("static_obs", "dyn_obs", "dyn_goal") else v[a:]).cpu().numpy()
+            want = st[key].view(np.int32) if key == "episode" else st[key]
+            np.testing.assert_array_equal(got, want, err_msg=f"after step {t0}: state[{key}]")
+    assert n_trunc > 0
+    env.status()
+    env.close()
+
+
 def test_step_kernel_time_limit_boundary(gpu):
     """Every env starts at ep_len 995..999: the TimeLimit truncates the survivors within five
     steps and the autoreset starts their next episode (ep_len 999 -> done, ep_len 0)."""
