@@ -551,7 +551,7 @@ def config2_leg(args, gb, dev, rank, world, stream):
     res, kname = graph_steps_leg(gb, dev, rank, world, stream, N, W, args.config2_steps, args.settle)
     res["workload"] = (f"BASELINE config 2: BallEnv step + prep_state4, random actions, {N} envs/GPU, W=5, 13 static "
                        "+ 5 dynamic obstacles, TimeLimit 1000, autoreset, hipGraph replay of be_step launches")
-    add_measured(res["roofline"], committed_pmc("r03_pmc_config2.json", kname, N), res["kernel_us_mean"])
+    add_measured(res["roofline"], committed_pmc("r04_pmc_config2.json", kname, N), res["kernel_us_mean"])
     return res
 
 
@@ -584,7 +584,7 @@ def large_batch_leg(args, gb, dev, rank, world, stream):
                                  chunk=args.large_steps)
     res["workload"] = (f"the headline step at {N} envs/GPU, W={W} (working set past the Infinity Cache), "
                        "hipGraph replay of be_step launches")
-    add_measured(res["roofline"], committed_pmc("r03_pmc_large_batch.json", kname, N), res["kernel_us_mean"])
+    add_measured(res["roofline"], committed_pmc("r04_pmc_large_batch.json", kname, N), res["kernel_us_mean"])
     return res
 
 
@@ -699,7 +699,7 @@ def board_leg(args, gb, dev, rank, world, stream):
                        "random actionArray moves, autoreset, hipGraph replay",
            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
            "kernel_us_mean": ms * 1e3, "bytes_per_env_step": B, "achieved_GBs": B * N / (ms * 1e-3) / 1e9}
-    res["roofline"] = board_roofline(B, N, ms * 1e3, committed_pmc("r03_pmc_board_step.json", "board_kernel<6, false", N))
+    res["roofline"] = board_roofline(B, N, ms * 1e3, committed_pmc("r04_pmc_board_step.json", "board_kernel<6, false", N))
     del g
     # the same rollout fused: be_board_rollout, 100 steps per launch with the state in registers
     Kc = min(100, T)
@@ -735,7 +735,7 @@ def board_leg(args, gb, dev, rank, world, stream):
     Bf = 1 + 8 + 2 + 80 + (2 * 44 + 28 + 24) / Kc
     res["fused"]["bytes_per_env_step"] = Bf
     res["fused"]["roofline"] = board_roofline(Bf, N, res["fused"]["kernel_us_per_step"],
-                                              committed_pmc("r03_pmc_board_rollout.json", "board_kernel<6, true",
+                                              committed_pmc("r04_pmc_board_rollout.json", "board_kernel<6, true",
                                                             N * Kc))
     b.close()
     return res
