@@ -1,0 +1,61 @@
+"""The bench's method, checked: be_step launches captured into hipGraphs (torch.cuda.graph on a
+side stream, as bench.py's graph_steps_leg does) and replayed give the same trajectory as the same
+steps called eagerly -- every step's outputs, the final state and the stats slots, bit for bit --
+for each fixed-shape step kernel the BASELINE configs run."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import KEYS, make_env, np_state
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("W,N", [(10, 65536), (5, 4096), (10, 131072), (10, 32768)])
+def test_graph_replayed_steps_equal_eager(gpu, W, N):
+    from gym_ballenv_amd import _abi
+    from gym_ballenv_amd.config import EnvConfig
+    T, chunk = 60, 25
+    cfg_py = EnvConfig(time_limit=40)   # truncations and autoresets inside the captured steps
+    eager, graphed = (make_env(cfg_py, N, W, gpu, seed=123) for _ in range(2))
+    acts = eager.sample_actions(T, seed=7)
+    for e in (eager, graphed):
+        e.reset()
+    # per-step outputs of the graphed env: copied inside the graph after each step
+    rec = {k: torch.empty((T,) + tuple(getattr(graphed, k).shape), dtype=getattr(graphed, k).dtype, device=gpu)
+           for k in ("obs", "reward", "done", "truncated")}
+    lib, ctx, st, out = graphed._lib, graphed._ctx, C.byref(graphed._st), C.byref(graphed._out)
+    side = torch.cuda.Stream(gpu)
+    graphs = []
+    for c0 in range(0, T, chunk):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            cs = C.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+            for t in range(c0, min(T, c0 + chunk)):
+                rc = lib.be_step(ctx, st, C.c_void_p(acts[t].data_ptr()), None, None, out, cs)
+                if rc:
+                    _abi.check(rc, ctx)
+                for k, buf in rec.items():
+                    buf[t].copy_(getattr(graphed, k))
+        graphs.append(g)
+    for g in graphs:
+        g.replay()
+    torch.cuda.synchronize(gpu)
+    n_done = 0
+    for t in range(T):
+        obs, reward, done, info = eager.step(acts[t])
+        n_done += int(done.sum())
+        for k, v in (("obs", obs), ("reward", reward), ("done", done), ("truncated", info["truncated"])):
+            assert torch.equal(rec[k][t], v), f"{k} t={t}"
+    torch.cuda.synchronize(gpu)
+    a, b = np_state(eager), np_state(graphed)
+    for k in KEYS:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert torch.equal(eager.stats_buf, graphed.stats_buf)
+    assert n_done > 0
+    assert eager.kernel_name("step") == graphed.kernel_name("step")
+    for e in (eager, graphed):
+        e.status()
+        e.close()
