@@ -1,7 +1,7 @@
 """The bench's method, checked: be_step launches captured into hipGraphs (torch.cuda.graph on a
 side stream, as bench.py's graph_steps_leg does) and replayed give the same trajectory as the same
 steps called eagerly -- every step's outputs, the final state and the stats slots, bit for bit --
-for each fixed-shape step kernel the BASELINE configs run."""
+for each fixed-shape step kernel the BASELINE configs run, and for the createBoard step."""
 import ctypes as C
 
 import numpy as np
@@ -59,3 +59,40 @@ def test_graph_replayed_steps_equal_eager(gpu, W, N):
     for e in (eager, graphed):
         e.status()
         e.close()
+
+
+def test_graph_replayed_board_steps_equal_eager(gpu):
+    """The createBoard leg's method: be_board_step captured and replayed == eager steps (features,
+    reward, done, truncated per step, final state), 65 536 envs, 6 statics, autoreset, a short
+    TimeLimit so resets happen inside the graph."""
+    from gym_ballenv_amd import BatchedBoard
+    N, T = 65536, 60
+    eager, graphed = (BatchedBoard(N, 6, device=gpu, seed=0xB0A2D, autoreset=True, time_limit=30) for _ in range(2))
+    gen = torch.Generator(device=gpu).manual_seed(3)
+    acts = torch.randint(0, 4, (T, N), dtype=torch.uint8, device=gpu, generator=gen)
+    for b in (eager, graphed):
+        b.reset()
+    rec = {k: torch.empty((T,) + tuple(getattr(graphed, k).shape), dtype=getattr(graphed, k).dtype, device=gpu)
+           for k in ("features", "reward", "done", "truncated")}
+    side = torch.cuda.Stream(gpu)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        sp = C.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+        for t in range(T):
+            graphed._lib.be_board_step(graphed._h, C.byref(graphed._st), C.c_void_p(acts[t].data_ptr()), None,
+                                       C.byref(graphed._out), sp)
+            for k, buf in rec.items():
+                buf[t].copy_(getattr(graphed, k))
+    g.replay()
+    torch.cuda.synchronize(gpu)
+    n_done = 0
+    for t in range(T):
+        f, r, d, info = eager.step(acts[t])
+        n_done += int(d.sum())
+        for k, v in (("features", f), ("reward", r), ("done", d), ("truncated", info["truncated"])):
+            assert torch.equal(rec[k][t], v), f"{k} t={t}"
+    for k in eager.STATE_KEYS:
+        assert torch.equal(getattr(eager, k), getattr(graphed, k)), k
+    assert n_done > 0
+    for b in (eager, graphed):
+        b.close()
