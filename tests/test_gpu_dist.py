@@ -6,7 +6,8 @@ steps its shard() of the global batch (8 192, or config 4's 262 144) for 120 / 4
 env id, so goal changes and TimeLimit truncations happen) and all_gathers its stats record.
 This process then runs the whole batch on one rank and checks, bit for bit, that the ranks'
 per-env rewards / dones / obs, their final states, their per-wave stats slots and the gathered
-records equal the matching rows of the one-rank run (Philox streams are keyed by global env id).
+records equal the matching rows of the one-rank run (Philox streams are keyed by global env id),
+and that the last rank's last 1 024 envs equal the oracle run on the same global ids.
 """
 import os
 import socket
@@ -96,4 +97,26 @@ def test_multi_rank_engine_matches_one_rank(gpu, tmp_path, E, T, world):
     assert comb["max_return"] == one["max_return"]
     assert comb["mean_length"] == pytest.approx(one["mean_length"], rel=1e-12)
     assert comb["mean_return"] == pytest.approx(one["mean_return"], rel=1e-12)
+
+    # not only a self-comparison: the last rank's last 1 024 envs against the oracle, step by step
+    from oracle import oracle
+    rk = ranks[-1]
+    off, n = int(rk["off"]), int(rk["n"])
+    k = 1024
+    a = off + n - k
+    cfg = gb.EnvConfig().to_abi(k, W, env_offset=a, seed=seed)
+    ost = oracle.new_state(cfg)
+    oout = oracle.new_out(cfg)
+    oracle.reset(cfg, ost, oout)
+    ost["ep_len"][:] = start_lens(a, k).numpy()
+    loc = slice(a - off, a - off + k)
+    for t in range(T):
+        oracle.step(cfg, ost, oout, actions=acts[t, a:a + k].cpu().numpy())
+        np.testing.assert_array_equal(rk["reward"][t, loc], oout["reward"], err_msg=f"oracle reward t={t}")
+        np.testing.assert_array_equal(rk["done"][t, loc], oout["done"].astype(bool), err_msg=f"oracle done t={t}")
+        np.testing.assert_array_equal(rk["obs_bits"][t, loc], np.packbits(oout["obs"], axis=1), err_msg=f"oracle obs t={t}")
+    for key in ("agent", "goal", "ep_len", "static_obs", "dyn_obs", "dyn_goal"):
+        got = rk["state_" + key]
+        got = got[:, loc] if key in ("static_obs", "dyn_obs", "dyn_goal") else got[loc]
+        np.testing.assert_array_equal(got, ost[key], err_msg=f"oracle state[{key}]")
     env.close()
