@@ -1858,8 +1858,10 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
 //    wave's LDS stage, and the wave copies its 64/L rows (a contiguous 232 / 464 B) out;
 //  * autoreset is wave_resets (the owner is the group's lane 0), as in step2_kernel;
 //  * the block's 32 envs share one stats slot: every wave leaves its finished envs' return and
-//    length in LDS after the physics, and after a block barrier wave 0 folds them in env order --
-//    the same sums, in the same order, as the one-lane kernel.
+//    length in LDS after the physics, and after a block barrier at the very end (behind every
+//    wave's obs stores: 4.01 against 4.03 us with the barrier right after the physics,
+//    profiles/r04_stepw_late_fold_ab.txt) wave 0 folds them in env order -- the same sums, in
+//    the same order, as the one-lane kernel.
 template <int L>
 __device__ __forceinline__ uint32_t lane_group_or(uint32_t x) {   // OR over the aligned group of L lanes
   static_assert(L == 4 || L == 8, "L must be 4 or 8");
@@ -2041,24 +2043,11 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     if (lane == 0) atomicOr(p.status, (int)f);
   }
   // ---- the block's stats slot (32 envs): every wave leaves its finished envs' return / length in
-  //      LDS right after the physics, one block barrier, and wave 0 folds the 32 in env order
-  //      before its obs work (the waves reach the barrier together: the same chain)
+  //      LDS right after the physics (before a reset overwrites ret / len); the fold is at the end
   if (slot && !DBG(DBG_NO_STATS)) {
     const bool fin = done && valid;   // (the same on every lane of the group: they all write it)
     s_fin[el] = fin ? 1 : 0;
     if (fin && h == 0) { s_fret[el] = ret; s_flen[el] = len; }
-    __syncthreads();
-    if (w == 0) {
-      const bool d = lane < 32 && s_fin[lane & 31];
-      if (__ballot(d)) {
-        const WaveStats ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
-        if (lane == 0) {
-          reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
-          reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
-          reinterpret_cast<double2*>(slot)[2] = make_double2(fmin(sp2.x, ws.mn), fmax(sp2.y, ws.mx));
-        }
-      }
-    }
   }
   PH(4);
   if (DBG(DBG_EXIT_PHYSICS)) return;
@@ -2146,6 +2135,22 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
       for (int b = lane; b < nb; b += 64) {
         if (p.obs) p.obs[(size_t)e0u * F + b] = stage[b];
         if (p.obs_f32) p.obs_f32[(size_t)e0u * F + b] = (float)stage[b];
+      }
+    }
+  }
+  // ---- the block's stats slot (32 envs), folded after every wave's obs stores are issued: one
+  //      block barrier, then wave 0 folds the 32 finished flags / returns / lengths in env order
+  if (slot && !DBG(DBG_NO_STATS)) {
+    __syncthreads();
+    if (w == 0) {
+      const bool d = lane < 32 && s_fin[lane & 31];
+      if (__ballot(d)) {
+        const WaveStats ws = wave_stats(d, d ? s_fret[lane & 31] : 0.0, d ? s_flen[lane & 31] : 0);
+        if (lane == 0) {
+          reinterpret_cast<double2*>(slot)[0] = make_double2(sp0.x + ws.n, sp0.y + ws.s1);
+          reinterpret_cast<double2*>(slot)[1] = make_double2(sp1.x + ws.s2, sp1.y + ws.sl);
+          reinterpret_cast<double2*>(slot)[2] = make_double2(fmin(sp2.x, ws.mn), fmax(sp2.y, ws.mx));
+        }
       }
     }
   }
