@@ -1882,7 +1882,9 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   static_assert(NDC <= 5, "one Philox block of 24-bit fields");
   static_assert(16 * KR >= (64 / (NSC + NDC)) * (KR + 4), "wave reset scratch");
   static_assert(WB % 8 == 0, "a wave's rows are whole 8-byte words");
-  __shared__ Tables t;
+  // one copy of the tables per wave, staged under a wave barrier: no block barrier at the start
+  // (3.97 against 4.01 us with one block copy, profiles/r04_stepw_wave_tables_ab.txt)
+  __shared__ Tables t_wave[NWAVE];
   __shared__ uint32_t s_rows[NWAVE][16 * KR];      // wave_resets scratch (row masks + stash)
   __shared__ __align__(16) uint8_t s_stage[NWAVE][SW];
   __shared__ double s_fret[32];
@@ -1897,13 +1899,14 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
   uint8_t* stage = &s_stage[w][0];
+  Tables& t = t_wave[w];
 
   // ---- every load, straight-line, in use order (as step2_kernel)
-  constexpr int TL = (TW + CT - 1) / CT;
+  constexpr int TL = (TW + 63) / 64;   // table words per lane
   uint32_t tword[TL];
 #pragma unroll
   for (int j = 0; j < TL; ++j)
-    tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid + j * CT, TW - 1));
+    tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(lane + j * 64, TW - 1));
   const uint32_t episode = ld_s(p.episode, ic);
   const int len0 = ld_s(p.ep_len, ic);
   const int32_t agent0 = ld_s(p.agent, ic), goal0 = ld_s(p.goal, ic);
@@ -1940,8 +1943,10 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
     sp2 = reinterpret_cast<const double2*>(slot)[2];
   }
 #pragma unroll
-  for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tid + j * CT, TW - 1)] = tword[j];
-  __syncthreads();   // tables staged
+  for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(lane + j * 64, TW - 1)] = tword[j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // this wave's copy staged
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (DBG(DBG_EXIT_BARRIER)) {   // diagnostics: the loads issued, nothing else
     if (valid && (agent0 ^ goal0 ^ so[0] ^ dp[0] ^ len0 ^ a ^ (int)old_dist ^ (int)ret) == 0x7fffffff) p.obs[i] = 1;
     return;

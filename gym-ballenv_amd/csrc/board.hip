@@ -573,11 +573,16 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   // (steps, N, ...) rows; modes 0 / 1 are one pass of the same body
   const int steps = ROLL ? p.steps : 1;   // ROLL: the mode-3 instantiation
   // the action table in LDS (a table read from memory is a second load on the move's chain), and
-  // the next step's action read one step ahead in the fused rollout, so its latency overlaps a step
-  __shared__ double s_act[2 * BE_BOARD_MAX_ACTIONS];
+  // the next step's action read one step ahead in the fused rollout, so its latency overlaps a step.
+  // One copy per wave under a wave barrier, no block barrier (step 8.08-8.12 against 8.10-8.16 us,
+  // fused 2.96-3.05 against 3.05-3.08: profiles/r04_board_wave_actions_ab.txt)
+  __shared__ double s_act_w[4][2 * BE_BOARD_MAX_ACTIONS];
+  double* s_act = &s_act_w[w][0];
   if (p.mode != 1 && p.actions) {   // (uniform)
-    if (threadIdx.x < 2 * p.num_actions) s_act[threadIdx.x] = (&p.tables->actions[0][0])[threadIdx.x];
-    __syncthreads();
+    if (lane < 2 * p.num_actions) s_act[lane] = (&p.tables->actions[0][0])[lane];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   int a_pf = 0;
   double dx_pf = 0.0, dy_pf = 0.0;
