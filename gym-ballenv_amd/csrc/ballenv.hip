@@ -1575,7 +1575,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   static_assert(NDC <= 5, "one Philox block of 24-bit fields");
   static_assert(16 * KR >= (64 / (NSC + NDC)) * (KR + 4), "wave reset scratch");
   extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ Tables t;
+  __shared__ Tables t_wave[NWAVE];               // one copy of the tables per wave (no block barrier)
   __shared__ uint32_t s_rows[NWAVE][16 * KR];    // wave_resets scratch (row masks + stash)
   constexpr int TW = (int)(sizeof(Tables) / 4);
 
@@ -1587,9 +1587,10 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
   NearList<CT> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
+  Tables& t = t_wave[w];
   uint8_t* stage = stage_blk + (size_t)w * EPW * F;   // the wave's 32 rows
-  constexpr int TB = CT;     // the block stages one copy of the tables
-  const int tt0 = tid;
+  constexpr int TB = 64;     // each wave stages its own copy of the tables
+  const int tt0 = lane;
 
   // ---- every load, straight-line, in use order (32-bit element offsets from uniform bases;
   //      obstacle k of lane h at element k*N + env: pick_kernel keeps NS*N < 2^30)
@@ -1630,10 +1631,12 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   }
 #pragma unroll
   for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tt0 + j * TB, TW - 1)] = tword[j];
-  // the only block barrier: tables staged (state loads retire in order as used).  A per-wave copy
-  // of the tables without this barrier measured the same (6.57 vs 6.56 us), as did a scheduling
-  // barrier pinning it and loading the f64s before the obstacles
-  __syncthreads();
+  // this wave's copy of the tables staged (state loads retire in order as used): a wave barrier, no
+  // block barrier in the kernel -- 6.38-6.40 against 6.45-6.46 us with one block copy under a block
+  // barrier (profiles/r04_step2_wave_tables_ab.txt; round 2 had measured the two the same)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   DIAG(1);
   if (DBG(DBG_EXIT_BARRIER)) return;
   if (DBG(DBG_WAIT_LOADS)) {   // diagnostics: when has every load of this wave landed?
