@@ -941,7 +941,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   constexpr bool COOP = WT > 0;                   // cooperative reset path (needs compile-time W)
   constexpr int KR = WT > 0 ? Geo<WT>::K : 1;
   extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ Tables t;
+  // FIXED: one copy of the tables per wave, so the fixed-shape kernel has no block barrier (8.11-8.21
+  // against 8.15-8.27 us at 131 072 envs, the same within noise at 262 144 and 2^20 envs:
+  // profiles/r04_onelane_wave_tables_ab.txt)
+  __shared__ Tables t_blk[FIXED ? BLOCK_THREADS / 64 : 1];
   __shared__ WaveStats s_ws[BLOCK_THREADS / 64];
   __shared__ int s_nreset;
   __shared__ int16_t s_slot_of[EPB];               // env -> reset slot (-1: none)
@@ -956,6 +959,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   if (DBG(DBG_EXIT_ENTRY)) return;
   const int N = p.n, Ns = FIXED ? NSC : p.ns, Nd = FIXED ? NDC : p.nd;
   const int tid = threadIdx.x;
+  Tables& t = t_blk[FIXED ? (tid >> 6) : 0];
   const int q = tid & (LPE - 1);                  // lane within the env's group
   const int el = tid / LPE;                        // env within the block
   const int blk0 = (int)blockIdx.x * EPB;
@@ -989,14 +993,19 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   for (int j = 0; j < SPL; ++j) so[j] = 0;
 #pragma unroll
   for (int j = 0; j < DPL; ++j) { dp[j] = 0; dgi[j] = 0; t0[j] = 0; t1[j] = 0; }
-  uint32_t tword = 0u;
+  constexpr int TLW = FIXED ? (TW + 63) / 64 : 1;   // table words per lane
+  uint32_t tword[TLW];
+#pragma unroll
+  for (int j = 0; j < TLW; ++j) tword[j] = 0u;
   if constexpr (FIXED) {
     // straight-line prologue (no branches around loads, clamped env index; invalid lanes
     // never store): the waitcnt pass can then retire the loads one by one -- tables
     // first, then in use order -- instead of draining everything at the first join
     // (32-bit unsigned element offsets from uniform bases: global_load's SGPR-base form)
     const uint32_t ic = (uint32_t)min(i, N - 1);
-    tword = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tid, TW - 1));
+#pragma unroll
+    for (int j = 0; j < TLW; ++j)
+      tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min((tid & 63) + j * 64, TW - 1));
     episode = ld_s(p.episode, ic);
     len0 = ld_s(p.ep_len, ic);
     a = ld_s(p.actions, ic);
@@ -1010,7 +1019,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     total = ld_s(p.total_dist, ic);
     ret = ld_s(p.ep_return, ic);
   } else {
-  tword = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
+  tword[0] = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
   if (valid) {
     // issue order = use order: vmcnt retires loads in order, so the Philox draws (keyed by
     // episode, ep_len) and the obstacle moves start while the statics and f64s are in flight
@@ -1043,10 +1052,18 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     }
   }
   }
-  if (FIXED || tid < TW) reinterpret_cast<uint32_t*>(&t)[FIXED ? min(tid, TW - 1) : tid] = tword;
-  if (EPB == BLOCK_THREADS || tid < EPB) s_slot_of[tid] = -1;
-  if (tid == 0) s_nreset = 0;
-  __syncthreads();  // barrier 1: tables staged (the state loads retire in order as they are used)
+  if constexpr (FIXED) {   // this wave's copy of the tables; nothing else is block-shared here
+#pragma unroll
+    for (int j = 0; j < TLW; ++j) reinterpret_cast<uint32_t*>(&t)[min((tid & 63) + j * 64, TW - 1)] = tword[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    if (tid < TW) reinterpret_cast<uint32_t*>(&t)[tid] = tword[0];
+    if (EPB == BLOCK_THREADS || tid < EPB) s_slot_of[tid] = -1;
+    if (tid == 0) s_nreset = 0;
+    __syncthreads();  // barrier 1: tables staged (the state loads retire in order as they are used)
+  }
   DIAG(1);
   if (DBG(DBG_WAIT_LOADS)) {   // diagnostics: when has every load of this wave landed?
     __builtin_amdgcn_s_waitcnt(0);   // vmcnt(0) expcnt(0) lgkmcnt(0)
