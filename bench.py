@@ -90,6 +90,12 @@ def parse():
                         "at --envs and at --large-envs (0 = skip)")
     p.add_argument("--from-reset-steps", type=int, default=400,
                    help="the headline step timed straight from a fresh reset (no settle): timed steps (0 = skip)")
+    p.add_argument("--shard-steps", type=int, default=1000,
+                   help="config 4's per-rank shards (131072 / 65536 / 32768 envs = the N = 2 / 4 / 8 split) timed on "
+                        "one GPU, N = 1 only: timed steps per shard (0 = skip)")
+    p.add_argument("--eager-steps", type=int, default=1000,
+                   help="the drop-in as its caller drives it: BatchedBallEnv.step(actions) called from Python per "
+                        "step, no graph (examples/ball_cnn_ac3.py:588 for every env): timed calls (0 = skip)")
     return p.parse_args()
 
 
@@ -189,6 +195,12 @@ def board_cpu_baseline(seconds, procs=None, static_obstacles=6):
                       "done / 1000 steps (oracle/py_board.py, pure Python + numpy)"}
 
 
+def gb_step_bytes(env):
+    """be_step_bytes of an env's config: the bytes the engine's layout moves per env-step."""
+    import gym_ballenv_amd as gb
+    return gb.step_bytes(env.cfg, env.window)
+
+
 def timed_graph_steps(graphs, steps, dev, stream, world):
     """Replay graphs (steps in total), bracketed by barrier + synchronize; max over ranks."""
     import torch
@@ -239,10 +251,11 @@ def cold_actions_leg(args, env, lib, dev, stream, world, B):
     el, ms = timed_graph_steps(graphs, T, dev, stream, world)
     del graphs, flush
     env.status()
-    return {"what": f"the headline step, {T} steps on a fresh action tape read from HBM (caches flushed by a "
-                    "512-MB write before the timed pass); the headline's rows are Infinity-Cache resident",
-            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
-            "kernel_us_mean": ms * 1e3, "frac": B * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    res = {"what": f"the headline step, {T} steps on a fresh action tape read from HBM (caches flushed by a "
+                   "512-MB write before the timed pass); the headline's rows are Infinity-Cache resident",
+           "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
+           "kernel_us_mean": ms * 1e3, "frac": B * N / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    return moved(res, gb_step_bytes(env), N, ms * 1e3, None)
 
 
 def policy_leg(args, gb, dev, rank, world, stream):
@@ -387,17 +400,18 @@ def policy_roofline(args, gb, dev, rank, pol, us_per_step, chunk, img):
                       "blocks are one block per CU, and the 89-KB policy image leaves LDS for only one): env "
                       "physics, select_action's softmax/draw and the head FMAs of the dense tiles"}
     # counters of the same kernel / envs / chunk (tools/pmc_passes.sh + tools/pmc_report.py, committed profile)
-    pmc = os.path.join(ROOT, "profiles", "r03_pmc_policy_rollout.json")
-    if os.path.exists(pmc):
-        d = json.load(open(pmc))
-        if d.get("units_per_dispatch") == N * chunk and f"rollout_kernel<{W}, 13, 5, {HT}, {KS}," in (d.get("kernel") or ""):
-            res.update({"traffic": d["hbm_bytes_per_dispatch"], "traffic_unit": f"HBM bytes per launch ({chunk} steps)",
-                        "traffic_per_env_step": d["hbm_bytes_per_unit"],
-                        "valu_active_frac": d.get("valu_active_per_simd_frac_est"),
-                        "mfma_busy_frac": d.get("mfma_busy_frac_est"),
-                        "lds_bank_conflict_frac": d.get("lds_bank_conflict_frac"),
-                        "wave_cycle_split": d.get("wave_cycle_split"),
-                        "pmc_source": "committed profile " + os.path.relpath(pmc, ROOT)})
+    d = newest_pmc("pmc_policy_rollout.json", f"rollout_kernel<{W}, 13, 5, {HT}, {KS},", N * chunk)
+    if d:
+        res.update({"traffic": d["hbm_bytes_per_dispatch"], "traffic_unit": f"HBM bytes per launch ({chunk} steps)",
+                    "traffic_per_env_step": d["hbm_bytes_per_unit"],
+                    "valu_active_frac": d.get("valu_active_per_simd_frac_est"),
+                    "mfma_busy_frac": d.get("mfma_busy_frac_est"),
+                    "lds_bank_conflict_frac": d.get("lds_bank_conflict_frac"),
+                    "wave_cycle_split": d.get("wave_cycle_split"),
+                    "pmc_source": d["source"]})
+    b = d["hbm_bytes_per_dispatch"] if d else B * N * chunk     # bytes one launch (chunk steps) moves
+    res.update({"moved_bytes_per_launch": b, "moved_source": d["source"] if d else "algorithmic (above)",
+                "moved_frac": b / (us_per_step * chunk * 1e-6) / 1e9 / HBM_PEAK_GBS})
     return res
 
 
@@ -458,15 +472,10 @@ def rollout_leg(args, gb, dev, rank, world, stream):
     # when they were taken on the kernel this run launched)
     kname = env.kernel_name("rollout")
     res["kernel"] = kname
-    for f in ("r02_pmc_rollout_kernel.json", "r01_pmc_rollout_kernel.json"):
-        pmc = os.path.join(ROOT, "profiles", f)
-        if not os.path.exists(pmc):
-            continue
-        d = json.load(open(pmc))
-        if d.get("units_per_dispatch") == N * Kc and f"::{kname}(" in (d.get("kernel") or ""):
-            res.update({"traffic_per_env_step": d["hbm_bytes_per_unit"],
-                        "traffic_source": "committed profile " + os.path.relpath(pmc, ROOT)})
-            break
+    d = newest_pmc("pmc_rollout_kernel.json", f"::{kname}(", N * Kc)
+    if d:
+        res.update({"traffic_per_env_step": d["hbm_bytes_per_unit"], "traffic_source": d["source"]})
+    moved(res, B, N * Kc, us_step * Kc, d, "algorithmic (above)")
     env.close()
     return res
 
@@ -477,7 +486,8 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
     (the headline's method), after `settle` untimed steps since reset (0: timed straight from
     the reset).  Envs are the global ids [env_offset, env_offset + N) (default rank * N: weak
     scaling); `global_envs` (strong scaling: a fixed batch split over the ranks) sets the
-    env-steps counted per step and adds the ranks' combined episode statistics (all_gather).
+    env-steps counted per step and adds the ranks' combined episode statistics (all_gather) of
+    the TIMED steps (the statistics slots are zeroed after the untimed settle replays).
     Returns (result dict, kernel name); the env is closed."""
     import ctypes as C
     import torch
@@ -508,6 +518,7 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
     if settle <= 0:
         env.reset()      # timed straight from a fresh reset (in place: the graphs' buffers)
         untimed = 0
+    env.clear_stats()    # in place (the graphs' stats pointer): episodes of the timed steps only
     torch.cuda.synchronize(dev)
     el, ms = timed_graph_steps(graphs, T, dev, stream, world)
     env.status()
@@ -530,18 +541,74 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
                         "engine_bytes_per_env_step": B_eng,
                         "engine_frac": B_eng * N / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                         "measured_frac": None}}
+    moved(res["roofline"], B_eng, N, us, None)    # legs with a committed profile re-run it (add_measured)
     if episodes is not None:
         res["episodes"] = episodes
     return res, kname
 
 
-def add_measured(rf, pmc, us):
-    """roofline.traffic / measured_frac from a committed PMC profile (bytes per launch)."""
+def add_measured(rf, pmc, us, units):
+    """roofline.traffic / measured_frac from the newest committed PMC profile (bytes per launch), and
+    moved_frac (PMC bytes, else the engine's be_step_bytes)."""
     if pmc:
         t = pmc["hbm_bytes_per_dispatch"]
         rf.update({"traffic": t, "measured_GBs": t / (us * 1e-6) / 1e9,
                    "measured_frac": t / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic_source": pmc["source"]})
-    return rf
+    return moved(rf, rf["engine_bytes_per_env_step"], units, us, pmc)
+
+
+def eager_step_leg(args, gb, dev, rank, world, stream, graph_kernel_us):
+    """The drop-in as its caller drives it (examples/ball_cnn_ac3.py:553-613, env.step at :588, for
+    every env): BatchedBallEnv.step(actions) called from Python once per step, no graph; each step's
+    actions come from one torch op (random_ into a preallocated (N,) u8 buffer), as a policy's
+    output would.  Reported: host microseconds per step() call (the Python + ctypes + HIP launch
+    cost of the call itself), host microseconds per loop iteration (the action op included), GPU
+    microseconds per iteration (events around the loop: the action op's kernel + be_step + gaps),
+    and env-steps/s of the whole loop beside the graph-replayed headline kernel time."""
+    import torch
+    N, W, T = args.envs, args.window, args.eager_steps
+    env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
+    env.reset()
+    acts = torch.empty(N, dtype=torch.uint8, device=dev)
+    for _ in range(max(args.settle, 50)):           # untimed: past the post-reset transient, caches warm
+        acts.random_(0, 9)
+        env.step(acts)
+    env.status()
+    call = 0.0
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if DIST_ON:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    pc = time.perf_counter
+    ev0.record(stream)
+    t0 = pc()
+    for _ in range(T):
+        acts.random_(0, 9)
+        c0 = pc()
+        env.step(acts)
+        call += pc() - c0
+    t_issue = pc() - t0
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    el = pc() - t0
+    if DIST_ON:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    env.status()
+    gpu_us = ev0.elapsed_time(ev1) * 1e3 / T
+    res = {"workload": f"BatchedBallEnv.step(actions) from Python, {N} envs/GPU, W={W}, one call per step (no "
+                       "graph), actions from acts.random_(0, 9) into a preallocated u8 buffer each step",
+           "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3, "steps": T,
+           "host_us_per_step_call": call / T * 1e6, "host_us_per_iteration": t_issue / T * 1e6,
+           "gpu_us_per_iteration": gpu_us, "graph_replayed_step_kernel_us": graph_kernel_us,
+           "kernel": env.kernel_name("step"),
+           "host_call_over_kernel": (call / T * 1e6) / graph_kernel_us,
+           "bound": "host (the GPU waits on the calls)" if t_issue / T * 1e6 >= 0.9 * gpu_us else "gpu"}
+    env.close()
+    return res
 
 
 def config2_leg(args, gb, dev, rank, world, stream):
@@ -551,7 +618,7 @@ def config2_leg(args, gb, dev, rank, world, stream):
     res, kname = graph_steps_leg(gb, dev, rank, world, stream, N, W, args.config2_steps, args.settle)
     res["workload"] = (f"BASELINE config 2: BallEnv step + prep_state4, random actions, {N} envs/GPU, W=5, 13 static "
                        "+ 5 dynamic obstacles, TimeLimit 1000, autoreset, hipGraph replay of be_step launches")
-    add_measured(res["roofline"], committed_pmc("r04_pmc_config2.json", kname, N), res["kernel_us_mean"])
+    add_measured(res["roofline"], newest_pmc("pmc_config2.json", kname, N), res["kernel_us_mean"], N)
     return res
 
 
@@ -571,9 +638,42 @@ def config4_leg(args, gb, dev, rank, world, stream):
                        f"split over {world} rank(s) ({n} envs on rank {rank}), 13 static + 5 dynamic obstacles, "
                        "TimeLimit 1000, autoreset, hipGraph replay of be_step launches; stats all_gather after the "
                        "timed region")
-    res.update({"global_envs": G, "envs_per_rank": n, "ranks": world, "scaling": "strong"})
-    add_measured(res["roofline"], committed_pmc(f"r04_pmc_config4_{n}.json", kname, n), res["kernel_us_mean"])
+    res.update({"global_envs": G, "envs_per_rank": n, "ranks": world, "scaling": "strong",
+                "episodes_note": "episodes finished during the timed steps (all ranks)"})
+    add_measured(res["roofline"], newest_pmc(f"pmc_config4_{n}.json", kname, n), res["kernel_us_mean"], n)
+    if world == 1 and args.shard_steps > 0:
+        res["shards"] = config4_shards(args, gb, dev, stream, res)
     return res
+
+
+def config4_shards(args, gb, dev, stream, one):
+    """The 1 -> 8 GPU curve of config 4 predicted on one GPU: each per-rank shard of the 2/4/8-GPU
+    split (131 072 / 65 536 / 32 768 envs) stepped exactly as that rank would -- the LAST rank's
+    global ids (contiguous shard(), the highest ids), 1000 graph-replayed be_step launches after the
+    settle.  Ranks share nothing per step (no collective), so a rank's step time at N GPUs is its
+    shard's one-GPU time, and the node rate is projected as global envs / shard ms per step.
+    `one` is the 262 144-env leg on this GPU (the N = 1 point)."""
+    from gym_ballenv_amd.distributed import shard
+    G, W = args.config4_envs, 10
+    out = {"what": "config 4's per-rank shards on one GPU (last rank's global ids, graph-replayed be_step "
+                   "launches); projected node rate = global envs / shard ms per step (no per-step collective)",
+           "one_gpu": {"envs": G, "kernel": one["kernel"], "kernel_us_mean": one["kernel_us_mean"],
+                       "ms_per_step": one["ms_per_step"], "value": one["value"]}}
+    rows = []
+    for ranks in (2, 4, 8):
+        off, n = shard(G, ranks - 1, ranks)
+        r, kname = graph_steps_leg(gb, dev, 0, 1, stream, n, W, args.shard_steps, args.settle, env_offset=off)
+        rf = add_measured(r["roofline"], newest_pmc(f"pmc_config4_{n}.json", kname, n), r["kernel_us_mean"], n)
+        proj = G / (r["ms_per_step"] * 1e-3)
+        rows.append({"gpus": ranks, "envs_per_rank": n, "env_offset": off, "kernel": kname,
+                     "kernel_us_mean": r["kernel_us_mean"], "ms_per_step": r["ms_per_step"],
+                     "frac": rf["frac"], "moved_frac": rf["moved_frac"], "measured_frac": rf["measured_frac"],
+                     "traffic_source": rf.get("traffic_source"), "moved_source": rf["moved_source"],
+                     "projected_node_env_steps_per_s": proj,
+                     "projected_speedup_vs_1gpu": proj / one["value"],
+                     "projected_efficiency": proj / one["value"] / ranks})
+    out["by_gpus"] = rows
+    return out
 
 
 def large_batch_leg(args, gb, dev, rank, world, stream):
@@ -584,7 +684,7 @@ def large_batch_leg(args, gb, dev, rank, world, stream):
                                  chunk=args.large_steps)
     res["workload"] = (f"the headline step at {N} envs/GPU, W={W} (working set past the Infinity Cache), "
                        "hipGraph replay of be_step launches")
-    add_measured(res["roofline"], committed_pmc("r04_pmc_large_batch.json", kname, N), res["kernel_us_mean"])
+    add_measured(res["roofline"], newest_pmc("pmc_large_batch.json", kname, N), res["kernel_us_mean"], N)
     return res
 
 
@@ -627,8 +727,9 @@ def blocks_leg(args, gb, dev, rank, world, stream):
             ach = B * N / (ms * 1e-3) / 1e9
             leg[kind] = {"value": T * N * world / el, "unit": "env-rows/s", "kernel_us_mean": ms * 1e3,
                          "bytes_per_env": B,
-                         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                      "frac": ach / HBM_PEAK_GBS}}
+                         "roofline": moved({"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                            "frac": ach / HBM_PEAK_GBS}, B, N, ms * 1e3, None,
+                                           "algorithmic (exact: state read once, row written)")}
             del g
         env.status()
         env.close()
@@ -639,21 +740,49 @@ def blocks_leg(args, gb, dev, rank, world, stream):
     return res
 
 
-def committed_pmc(fname, kernel_sub, units):
-    """A committed tools/pmc_report.py profile, if it was taken on this kernel at this many units
-    per dispatch (else None)."""
-    path = os.path.join(ROOT, "profiles", fname)
-    if not os.path.exists(path):
-        return None
-    d = json.load(open(path))
-    if d.get("units_per_dispatch") != units or kernel_sub not in (d.get("kernel") or ""):
-        return None
-    d["source"] = "committed profile " + os.path.relpath(path, ROOT)
-    return d
+def newest_pmc(suffix, kernel_sub, units):
+    """The NEWEST committed PMC profile profiles/rNN_<suffix> (highest round first) taken on this
+    kernel at this many units per dispatch (tools/pmc_report.py / pmc_summary.py output), with
+    hbm_bytes_per_dispatch / units_per_dispatch normalised across the two formats; else None.
+    Older rounds' files of the same suffix are used only when no newer one matches the kernel."""
+    import glob
+    import re
+    found = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_" + suffix)):
+        m = re.match(r"r(\d\d)_", os.path.basename(path))
+        found.append((int(m.group(1)), path))
+    for rnd, path in sorted(found, reverse=True):
+        d = json.load(open(path))
+        u = d.get("units_per_dispatch", d.get("envs"))
+        if u != units or kernel_sub not in (d.get("kernel") or ""):
+            continue
+        d.setdefault("hbm_bytes_per_dispatch", d.get("hbm_bytes_per_launch"))
+        d.setdefault("hbm_bytes_per_unit", d["hbm_bytes_per_dispatch"] / units)
+        d["source"] = "committed profile " + os.path.relpath(path, ROOT)
+        return d
+    return None
+
+
+FRAC_NOTE = ("frac > 1: SURVEY 8(d)'s per-unit figure (390 B/env-step: int32 coordinates, a stored counter) is "
+             "more than this layout moves (be_step_bytes, 275 B); moved_frac is the bandwidth fraction of the "
+             "bytes actually moved")
+
+
+def moved(rf, B_eng, units, us, pmc, label="be_step_bytes (engine)"):
+    """roofline.moved_*: the bytes a launch actually moves -- the committed PMC traffic of this kernel
+    at this size when one exists (2 x FETCH_SIZE + WRITE_SIZE), else the engine's own algorithmic bytes
+    (be_step_bytes) -- per launch / kernel time / 8 TB/s, beside `frac` on the SURVEY figure; a `frac`
+    above 1 carries frac_note."""
+    b = pmc["hbm_bytes_per_dispatch"] if pmc else B_eng * units
+    rf.update({"moved_bytes_per_launch": b, "moved_source": pmc["source"] if pmc else label,
+               "moved_frac": b / (us * 1e-6) / 1e9 / HBM_PEAK_GBS})
+    if rf.get("frac") is not None and rf["frac"] > 1.0:
+        rf["frac_note"] = FRAC_NOTE
+    return rf
 
 
 def board_roofline(B, N, us, pmc):
-    """HBM roofline of a createBoard kernel plus its committed counters: f64-VALU work, not HBM."""
+    """HBM roofline of a createBoard kernel plus its newest committed counters: f64-VALU work, not HBM."""
     ach = B * N / (us * 1e-6) / 1e9
     r = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
          "traffic": None,
@@ -668,7 +797,7 @@ def board_roofline(B, N, us, pmc):
                              "dependencies) %.0f %% of its cycles; the work is f64 (featureExtractor: 7 correctly "
                              "rounded sqrt, 6 exp, acos, hypot per env-step)" % (100 * ws["SQ_ACTIVE_INST_VALU"],
                                                                                   100 * ws["SQ_WAIT_ANY"])})
-    return r
+    return moved(r, B, N, us, pmc, "algorithmic (above)")
 
 
 def board_leg(args, gb, dev, rank, world, stream):
@@ -699,7 +828,7 @@ def board_leg(args, gb, dev, rank, world, stream):
                        "random actionArray moves, autoreset, hipGraph replay",
            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
            "kernel_us_mean": ms * 1e3, "bytes_per_env_step": B, "achieved_GBs": B * N / (ms * 1e-3) / 1e9}
-    res["roofline"] = board_roofline(B, N, ms * 1e3, committed_pmc("r04_pmc_board_step.json", "board_kernel<6, false", N))
+    res["roofline"] = board_roofline(B, N, ms * 1e3, newest_pmc("pmc_board_step.json", "board_kernel<6, false", N))
     del g
     # the same rollout fused: be_board_rollout, 100 steps per launch with the state in registers
     Kc = min(100, T)
@@ -735,7 +864,7 @@ def board_leg(args, gb, dev, rank, world, stream):
     Bf = 1 + 8 + 2 + 80 + (2 * 44 + 28 + 24) / Kc
     res["fused"]["bytes_per_env_step"] = Bf
     res["fused"]["roofline"] = board_roofline(Bf, N, res["fused"]["kernel_us_per_step"],
-                                              committed_pmc("r04_pmc_board_rollout.json", "board_kernel<6, true",
+                                              newest_pmc("pmc_board_rollout.json", "board_kernel<6, true",
                                                             N * Kc))
     b.close()
     return res
@@ -845,6 +974,7 @@ def main():
         torch.cuda.synchronize(dev)
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    env.clear_stats()             # in place: `episodes` counts the timed steps' episodes only
     if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -887,18 +1017,15 @@ def main():
     achieved = B * N / (kern_ms * 1e-3) / 1e9                  # GB/s, algorithmic (§8(d)), per launch
     achieved_eng = B_eng * N / (kern_ms * 1e-3) / 1e9          # GB/s, engine bytes, per launch
 
-    # HBM-side bytes per launch from the committed PMC passes (tools/pmc_bench.sh):
+    # HBM-side bytes per launch from the newest committed PMC passes (tools/pmc_bench.sh):
     # 2 x FETCH_SIZE (gfx950 reports half of wide reads) + WRITE_SIZE, same kernel / envs / W
     # (committed profile, used only when it was taken on the kernel this run launched, same envs/W)
     kname = env.kernel_name("step")
-    traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
-    if os.path.exists(pmc):
-        d = json.load(open(pmc))
-        if d.get("envs") == N and d.get("window") == W and f"::{kname}(" in (d.get("kernel") or ""):
-            traffic, traffic_src = d.get("hbm_bytes_per_launch"), "committed profile " + os.path.relpath(pmc, ROOT)
+    pmc = newest_pmc("pmc_step_kernel.json", f"::{kname}(", N)
+    traffic, traffic_src = (pmc["hbm_bytes_per_dispatch"], pmc["source"]) if pmc else (None, None)
 
     cold_res = cold_actions_leg(args, env, lib, dev, stream, world, B) if args.cold_steps > 0 else None
+    eager_res = eager_step_leg(args, gb, dev, rank, world, stream, kern_ms * 1e3) if args.eager_steps > 0 else None
     c2_res = config2_leg(args, gb, dev, rank, world, stream) if args.config2_steps > 0 else None
     c4_res = config4_leg(args, gb, dev, rank, world, stream) if args.config4_steps > 0 else None
     large_res = large_batch_leg(args, gb, dev, rank, world, stream) if args.large_steps > 0 else None
@@ -937,6 +1064,7 @@ def main():
             "cpu_baseline": base,
             "episodes": ep,
             "cold_action_rows": cold_res,
+            "eager_step": eager_res,
             "config2": c2_res,
             "config4": c4_res,
             "large_batch": large_res,
@@ -946,6 +1074,8 @@ def main():
             "fused_rollout": roll_res,
             "blocks_obs": blocks_res,
         }
+        moved(line["roofline"], B_eng, N, kern_ms * 1e3, pmc)
+        line["episodes_note"] = "episodes finished during the timed steps (all ranks)"
         print(json.dumps(line), flush=True)
     env.close()
     if DIST_ON:

@@ -90,6 +90,14 @@ class BatchedBallEnv:
                                self.done.data_ptr(), self.truncated.data_ptr(), _ptr(self.terminal_obs),
                                self.final_return.data_ptr(), self.final_len.data_ptr(),
                                self.stats_buf.data_ptr() if self._track_stats else None)
+        # per-call constants of step(): the ctypes references and the info dict (its values are the
+        # same buffers every step), built once instead of on every call
+        self._st_ref, self._out_ref = C.byref(self._st), C.byref(self._out)
+        self._info = {"truncated": self.truncated, "final_return": self.final_return, "final_len": self.final_len}
+        if self.terminal_obs is not None:
+            self._info["terminal_obs"] = self.terminal_obs
+        self._obs_ret = self.obs_f32 if self._want_f32 else self.obs
+        self._a_ok = None       # the last actions tensor that passed step()'s checks as it was
 
     def _create_ctx(self):
         if self._ctx is not None:
@@ -103,9 +111,11 @@ class BatchedBallEnv:
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         _abi.check(self._lib.be_create(C.byref(self._abi_cfg), dev, C.byref(ctx)))
         self._ctx = ctx
+        self._dev_index = dev
 
     def _stream(self):
-        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        """The caller's current stream on this env's device (raw handle; no Stream object)."""
+        return C.c_void_p(torch._C._cuda_getCurrentRawStream(self._dev_index))
 
     # ------------------------------------------------------------------ gym surface
     @property
@@ -157,6 +167,29 @@ class BatchedBallEnv:
         draw_tape: (Nd, 2, N) int16 obstacle-move randint values (parity mode).
         Returns (obs, reward f64, done bool, info).
         """
+        if actions is not None and deltas is None and draw_tape is None:
+            # the common call (ball_cnn_ac3.py:588 for every env): the same (N,) u8 action buffer
+            # each step skips the re-checks -- one ctypes call, the info dict prebuilt (the host
+            # cost per call is bench.py's eager_step leg)
+            if (actions is not self._a_ok or actions.dtype != torch.uint8 or actions.shape != self._a_shape
+                    or actions.data_ptr() != self._a_ptr):
+                a = actions if actions.dtype == torch.uint8 else actions.to(torch.uint8)
+                if a.device != self.device:
+                    a = a.to(self.device)
+                a = a.contiguous()
+                self._check_shape(a, (self.num_envs,), "actions")
+                if a is not actions:          # a converted copy: keep it alive for the async launch
+                    self._keep = (a,)
+                    self._a_ok = None
+                else:
+                    self._a_ok, self._a_shape, self._a_ptr = a, a.shape, a.data_ptr()
+                ptr = a.data_ptr()
+            else:
+                ptr = self._a_ptr
+            rc = self._lib.be_step(self._ctx, self._st_ref, ptr, None, None, self._out_ref, self._stream())
+            if rc:
+                _abi.check(rc, self._ctx)
+            return self._obs_ret, self.reward, self.done, self._info
         a = d = t = None
         if actions is not None:
             a = actions if actions.dtype == torch.uint8 else actions.to(torch.uint8)
@@ -174,10 +207,7 @@ class BatchedBallEnv:
         _abi.check(self._lib.be_step(self._ctx, C.byref(self._st), _ptr(a), _ptr(d), _ptr(t),
                                      C.byref(self._out), self._stream()), self._ctx)
         self._keep = (a, d, t)
-        info = {"truncated": self.truncated, "final_return": self.final_return, "final_len": self.final_len}
-        if self.terminal_obs is not None:
-            info["terminal_obs"] = self.terminal_obs
-        return (self.obs_f32 if self._want_f32 else self.obs), self.reward, self.done, info
+        return self._obs_ret, self.reward, self.done, self._info
 
     def rollout(self, actions: torch.Tensor):
         """``K = actions.shape[0]`` consecutive steps in one launch (be_rollout).

@@ -801,6 +801,14 @@ __device__ __forceinline__ double reset_dists(int32_t ag, int32_t go, int32_t a0
 // esink(own, agent, goal, pre-resample agent) on the env's own lane, after a wave barrier.
 // LPE = 2 (step2_kernel): lanes 2e and 2e+1 share env e; m holds the even (owner) lanes, and
 // both lanes of a reset env take the new agent / goal / window rows (esink runs on both).
+// Ordering of a reset env's stores.  The physics stored the env's obstacles and scalars earlier
+// in the same launch, from the env's own lane(s); the sinks store the new values again, from
+// whichever lane drew them (osink: lane slot*G + k).  Both are vector stores of ONE wave, issued
+// in program order (the sinks after a wave barrier, the physics before it).  A wave's vector
+// memory instructions go through the CU's address / data path and the write-through L1 to the L2
+// channel of the address in issue order, so the later instruction's bytes win whichever lanes
+// issued the two: the same guarantee a lane relies on for its own two stores to one address
+// (the stores are sc1, none is an atomic).  The rule is per-wave program order, not per lane.
 template <int WT, int NSC, int NDC, int PMAX, class OSink, class ESink, int LPE = 1>
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
@@ -945,13 +953,17 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   // against 8.15-8.27 us at 131 072 envs, the same within noise at 262 144 and 2^20 envs:
   // profiles/r04_onelane_wave_tables_ab.txt)
   __shared__ Tables t_blk[FIXED ? BLOCK_THREADS / 64 : 1];
-  __shared__ WaveStats s_ws[BLOCK_THREADS / 64];
+  // block-cooperative reset list and block stats: the generic kernels only.  FIXED never
+  // initialises or reads them (it resets wave by wave through wave_resets and folds its stats per
+  // half-wave), so they are sized 1 there: a FIXED change that needs them must size them again.
+  constexpr int BLK_LIST = FIXED ? 1 : RCAP;
+  __shared__ WaveStats s_ws[FIXED ? 1 : BLOCK_THREADS / 64];
   __shared__ int s_nreset;
-  __shared__ int16_t s_slot_of[EPB];               // env -> reset slot (-1: none)
-  __shared__ int16_t s_reset_el[RCAP];
-  __shared__ uint32_t s_reset_ep[RCAP];
-  __shared__ int32_t s_reset_agent[RCAP], s_reset_goal[RCAP];
-  __shared__ uint32_t s_rows[RCAP][KR];
+  __shared__ int16_t s_slot_of[FIXED ? 1 : EPB];   // env -> reset slot (-1: none)
+  __shared__ int16_t s_reset_el[BLK_LIST];
+  __shared__ uint32_t s_reset_ep[BLK_LIST];
+  __shared__ int32_t s_reset_agent[BLK_LIST], s_reset_goal[BLK_LIST];
+  __shared__ uint32_t s_rows[RCAP][KR];            // FIXED too: 16 rows of wave_resets scratch per wave
   constexpr int TW = (int)(sizeof(Tables) / 4);
   static_assert(TW <= BLOCK_THREADS && sizeof(Tables) % 4 == 0, "table staging assumes <= 256 words");
 
@@ -1611,7 +1623,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
 
   // ---- every load, straight-line, in use order (32-bit element offsets from uniform bases;
   //      obstacle k of lane h at element k*N + env: pick_kernel keeps NS*N < 2^30)
-  constexpr int TL = (TW + TB - 1) / TB;   // table words per thread (1 at 256 threads)
+  constexpr int TL = (TW + TB - 1) / TB;   // table words per lane (each wave stages its own copy)
   uint32_t tword[TL];
 #pragma unroll
   for (int j = 0; j < TL; ++j)
@@ -1784,9 +1796,9 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
-      // both lanes take the new agent / goal / rows; each scalar is stored by the lane that stored
-      // it in the physics above (lane 1: ep_return / ep_len), so same-address stores stay in one
-      // lane's program order
+      // both lanes take the new agent / goal / rows; the scalars are split over the pair as in the
+      // physics above (lane 1: ep_return / ep_len).  Ordering against the physics stores is the
+      // wave's program order (wave_resets' note), whichever lane stores
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
       if (h) {
@@ -2097,9 +2109,9 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
-      // every lane of the group takes the new agent / goal / rows; each scalar is stored by the
-      // lane that stored it in the physics above (lane 0 agent, lane 1 ep_return / ep_len, lane 2
-      // prev_dist), so same-address stores stay in one lane's program order
+      // every lane of the group takes the new agent / goal / rows; the scalars are spread over the
+      // group as in the physics above (lane 0 agent, lane 1 ep_return / ep_len, lane 2 prev_dist).
+      // Ordering against the physics stores is the wave's program order (wave_resets' note)
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
       if (h == 0) {
@@ -3042,6 +3054,7 @@ struct be_ctx {
   int step5_lpe;       // W = 5: lanes per env of the fixed step kernel (1: be_kernel; 4 / 8: stepw_kernel)
   int roll5_lpe;       // W = 5: lanes per env of the fused rollout (1: rollout_kernel; 4 / 8: rolloutw_kernel)
   int max_lds;         // the device's LDS bytes per workgroup
+  Launch step_launch[2];   // be_step's kernel without / with the fixed-shape preconditions (fixed per context)
   int64_t blob_hdr[8]; // be_save_state's header (host memory that outlives the async copy)
   mutable struct { KFn fn; int lds; bool ok; } lds_cache[4];   // fits_lds() answers per (kernel, dynamic LDS)
   mutable std::mutex lds_mu;                                    // guards lds_cache (const entries may race)
@@ -3155,6 +3168,25 @@ int be_config_check(const be_config* c, char* msg, int32_t msg_len) {
            "action deltas out of range");
   BE_REQ(c->time_limit >= 0, "time_limit must be >= 0");
   BE_REQ(!(c->threshold_goal != c->threshold_goal), "threshold_goal is NaN");
+  {  // int16 coordinates.  The reference's dynamic obstacles are unbounded Python ints (no clamp,
+     // ballenv_env.py:334-347); here they are int16.  An obstacle spawns inside the obstacle strips
+     // and moves at most |speed| per axis per step, and with autoreset and a time limit an episode
+     // has at most time_limit moves, so the bound below holds for every episode and such a config
+     // can never leave int16.  Without that bound (time_limit 0, or autoreset 0: a caller may step
+     // past done) the kernels flag BE_STATUS_COORD_RANGE, the stored coordinate wraps (two's
+     // complement int16) and the caller must poll be_status.
+    int64_t ms = 0;
+    for (int k = 0; k < c->num_dynamic; ++k) ms = std::max<int64_t>(ms, std::abs((int64_t)c->obstacle_speed[k]));
+    const int64_t ex = std::max<int64_t>(std::abs((int64_t)c->strip_obs_x),
+                                         std::abs((int64_t)c->screen_width - c->strip_obs_x));
+    const int64_t ey = std::max<int64_t>(std::abs((int64_t)c->strip_obs_y),
+                                         std::abs((int64_t)c->screen_height - c->strip_obs_y));
+    BE_REQ(!(c->autoreset && c->time_limit > 0 && c->num_dynamic > 0) ||
+               std::max(ex, ey) + ms * (int64_t)c->time_limit <= 32767,
+           "dynamic obstacles can leave the int16 coordinate range within one episode: need "
+           "max spawn extent + max|obstacle_speed| * time_limit <= 32767 (or time_limit 0 / autoreset 0 "
+           "and poll status())");
+  }
 #undef BE_REQ
   if (msg && msg_len > 0) msg[0] = 0;
   return BE_OK;
@@ -3312,12 +3344,16 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
     while ((h + 1) * (h + 1) <= R * R - d * d) ++h;
     t.hw[d] = (uint8_t)h;
   }
-  hipError_t e = hipSetDevice(device);
+  const DeviceGuard dg(device);   // the caller's current device is restored on return
+  hipError_t e = dg.err;
   if (e == hipSuccess) e = hipMalloc(&ctx->status, sizeof(int));
   if (e == hipSuccess) e = hipMemset(ctx->status, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&ctx->d_tables, sizeof(Tables));
   if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, &ctx->tables, sizeof(Tables), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipDeviceSynchronize();
+  // be_step's two possible kernels, picked once (pick_kernel formats a name: not per launch)
+  ctx->step_launch[0] = pick_kernel(ctx->cfg, MODE_STEP, false, ctx->step_lanes, ctx->step5_lpe);
+  ctx->step_launch[1] = pick_kernel(ctx->cfg, MODE_STEP, true, ctx->step_lanes, ctx->step5_lpe);
   if (e != hipSuccess) {
     int rc = fail(nullptr, BE_E_HIP, "HIP error in be_create: %s", hipGetErrorString(e));
     if (ctx->status) (void)hipFree(ctx->status);
@@ -3331,6 +3367,7 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
 
 int be_destroy(be_ctx* ctx) {
   if (!ctx) return BE_OK;
+  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
   if (ctx->status) (void)hipFree(ctx->status);
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   delete ctx;
@@ -3369,10 +3406,10 @@ static int launch(be_ctx* ctx, int mode, KParams& a, void* stream, int32_t steps
                         ctx->unit_moves && ctx->distinct_goals;
   if (((uintptr_t)a.obs & 15) || ((uintptr_t)a.obs_f32 & 15))
     return fail(ctx, BE_E_INVALID, "%s", "obs / obs_f32 must be 16-byte aligned");
-  int cur = -1;
-  HIP_TRY(ctx, hipGetDevice(&cur));
-  if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
-  const Launch L = pick_kernel(ctx->cfg, mode, fixed_ok, ctx->step_lanes, ctx->step5_lpe);
+  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
+  HIP_TRY(ctx, dg.err);
+  const Launch L = mode == MODE_STEP ? ctx->step_launch[fixed_ok ? 1 : 0]
+                                     : pick_kernel(ctx->cfg, mode, fixed_ok, ctx->step_lanes, ctx->step5_lpe);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)L.threads);
   for (int32_t s = 0; s < steps; ++s) {
@@ -3435,9 +3472,8 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
   if (fits_lds(ctx, L)) {
     KParams a = make_params(ctx, st, out);
     a.actions = actions; a.steps = steps;
-    int cur = -1;
-    HIP_TRY(ctx, hipGetDevice(&cur));
-    if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
+    HIP_TRY(ctx, dg.err);
     const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)L.threads);
     hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
     HIP_TRY(ctx, hipGetLastError());
@@ -3469,9 +3505,8 @@ int be_internal_policy_rollout(be_ctx* ctx, const be_state* st, const be_pol_rol
   a.pol_bytes = r->img_bytes; a.pol_actions = r->num_actions; a.pol_img = r->img; a.pol_seed = r->seed;
   a.obs_in = r->obs_in; a.obs_last = r->obs_last;
   a.act_out = r->act->action; a.logp_out = r->act->log_prob; a.value_out = r->act->value;
-  int cur = -1;
-  HIP_TRY(ctx, hipGetDevice(&cur));
-  if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
+  HIP_TRY(ctx, dg.err);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
   hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
@@ -3494,9 +3529,8 @@ int be_observe(be_ctx* ctx, const be_state* st, const be_out* out, void* stream)
 int be_sample_actions(be_ctx* ctx, uint8_t* actions_out, int32_t steps, uint64_t seed, void* stream) {
   if (!ctx || !actions_out || steps < 0) return fail(ctx, BE_E_INVALID, "%s", "bad arguments to be_sample_actions");
   if (steps == 0) return BE_OK;
-  int cur = -1;
-  HIP_TRY(ctx, hipGetDevice(&cur));
-  if (cur != ctx->device) HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
+  HIP_TRY(ctx, dg.err);
   const int64_t total = (int64_t)ctx->cfg.num_envs * steps;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
@@ -3536,6 +3570,8 @@ int be_save_state(be_ctx* ctx, const be_state* st, void* blob, void* stream) {
   if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
   if (int rc = check_state(ctx, st)) return rc;
   if (!blob) return fail(ctx, BE_E_INVALID, "%s", "blob is NULL");
+  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
+  HIP_TRY(ctx, dg.err);
   const BlobLayout L = blob_layout(&ctx->cfg);
   blob_header(&ctx->cfg, L.total, ctx->blob_hdr);   // lives in the context: safe for an async copy
   hipStream_t s = (hipStream_t)stream;
@@ -3552,6 +3588,8 @@ int be_load_state(be_ctx* ctx, const be_state* st, const void* blob, void* strea
   if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
   if (int rc = check_state(ctx, st)) return rc;
   if (!blob) return fail(ctx, BE_E_INVALID, "%s", "blob is NULL");
+  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
+  HIP_TRY(ctx, dg.err);
   const BlobLayout L = blob_layout(&ctx->cfg);
   hipStream_t s = (hipStream_t)stream;
   int64_t got[8], want[8];
@@ -3570,6 +3608,8 @@ int be_load_state(be_ctx* ctx, const be_state* st, const void* blob, void* strea
 
 int be_status(be_ctx* ctx, int32_t* status_out, void* stream) {
   if (!ctx || !status_out) return fail(ctx, BE_E_INVALID, "%s", "bad arguments to be_status");
+  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
+  HIP_TRY(ctx, dg.err);
   HIP_TRY(ctx, hipStreamSynchronize((hipStream_t)stream));
   int v = 0;
   HIP_TRY(ctx, hipMemcpy(&v, ctx->status, sizeof v, hipMemcpyDeviceToHost));

@@ -45,6 +45,7 @@
 #include <string.h>
 
 #include "ballenv.h"
+#include "internal.h"
 #include "philox.h"
 
 namespace {
@@ -779,7 +780,8 @@ int be_board_create(const be_board_config* cfg, int32_t device, be_board** out) 
   BoardTables t;
   memset(&t, 0, sizeof t);
   for (int a = 0; a < cfg->num_actions; ++a) { t.actions[a][0] = cfg->actions[a][0]; t.actions[a][1] = cfg->actions[a][1]; }
-  hipError_t e = hipSetDevice(device);
+  const DeviceGuard dg(device);   // the caller's current device is restored on return
+  hipError_t e = dg.err;
   if (e == hipSuccess) e = hipMalloc(&b->status, sizeof(int));
   if (e == hipSuccess) e = hipMemset(b->status, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&b->d_tables, sizeof t);
@@ -797,6 +799,7 @@ int be_board_create(const be_board_config* cfg, int32_t device, be_board** out) 
 
 int be_board_destroy(be_board* b) {
   if (!b) return BE_OK;
+  const DeviceGuard dg(b->device);   // the caller's current device is restored on return
   if (b->status) (void)hipFree(b->status);
   if (b->d_tables) (void)hipFree(b->d_tables);
   delete b;
@@ -821,9 +824,8 @@ static int board_launch(be_board* b, const be_board_state* st, const be_board_ou
   if (mode == 3 && steps == 0) return BE_OK;
   if (mode == 2 && !out->features) return bfail(b, BE_E_INVALID, "be_board_observe needs out->features");
   if (tape && tape_len < 0) return bfail(b, BE_E_INVALID, "tape_len < 0");
-  int cur = -1;
-  hipError_t e = hipGetDevice(&cur);
-  if (e == hipSuccess && cur != b->device) e = hipSetDevice(b->device);
+  const DeviceGuard dg(b->device);   // the caller's current device is restored on return
+  hipError_t e = dg.err;
   if (e != hipSuccess) return bhip(b, e);
   const be_board_config& c = b->cfg;
   BParams p;
@@ -883,7 +885,9 @@ BE_DIAG_BOARD_ENTRIES   // diagnostics builds only (diag.h)
 
 int be_board_status(be_board* b, int32_t* status_out, void* stream) {
   if (!b || !status_out) return bfail(b, BE_E_INVALID, "bad arguments to be_board_status");
-  hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  const DeviceGuard dg(b->device);   // the caller's current device is restored on return
+  hipError_t e = dg.err;
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
   int v = 0;
   if (e == hipSuccess) e = hipMemcpy(&v, b->status, sizeof v, hipMemcpyDeviceToHost);
   const int zero = 0;

@@ -144,9 +144,8 @@ int be_observe_blocks(be_ctx* ctx, const be_state* st, uint8_t* out, float* out_
   if (int rc = be_ctx_check_state(ctx, st)) return rc;
   if (!out && !out_f32) return be_ctx_fail(ctx, BE_E_INVALID, "be_observe_blocks needs out or out_f32");
   const be_ctx_view cv = be_ctx_get(ctx);
-  int cur = -1;
-  hipError_t e = hipGetDevice(&cur);
-  if (e == hipSuccess && cur != cv.device) e = hipSetDevice(cv.device);
+  const DeviceGuard dg(cv.device);   // the caller's current device is restored on return
+  hipError_t e = dg.err;
   if (e != hipSuccess) return be_ctx_fail(ctx, BE_E_HIP, hipGetErrorString(e));
   BParams p{st->agent, st->goal, st->static_obs, st->dyn_obs, out, out_f32, cv.num_envs, cv.num_static, cv.num_dynamic};
   const size_t lds = 4 * (size_t)(out_f32 ? BLK_WAVE_F32 : BLK_WAVE_U8);

@@ -3,7 +3,29 @@
 #pragma once
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>
+
 #include "ballenv.h"
+
+// Makes `device` the calling thread's current HIP device for the scope of one entry point and
+// restores the caller's device on exit, so no be_* call changes which GPU later torch / HIP calls
+// of the same thread use (a one-process multi-device caller).  err != hipSuccess: the switch failed
+// (nothing to restore).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int device) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != device) err = hipSetDevice(device);
+    else prev = -1;                        // already current (or the query failed): nothing to restore
+    if (err != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
 
 struct be_ctx_view {
   int32_t num_envs, window, device, num_static, num_dynamic;

@@ -258,12 +258,6 @@ static int pol_hip_fail(be_ctx* ctx, hipError_t e) {
   return be_ctx_fail(ctx, BE_E_HIP, buf);
 }
 
-static int pol_set_device(be_ctx* ctx, int device) {
-  int cur = -1;
-  POL_TRY(ctx, hipGetDevice(&cur));
-  if (cur != device) POL_TRY(ctx, hipSetDevice(device));
-  return BE_OK;
-}
 
 struct be_policy {
   be_ctx* ctx;
@@ -303,7 +297,8 @@ int be_policy_create(be_ctx* ctx, int32_t hidden, int32_t num_actions, be_policy
     delete pol;
     return be_ctx_fail(ctx, BE_E_INVALID, "packed policy exceeds the LDS budget");
   }
-  int rc = pol_set_device(ctx, cv.device);
+  const DeviceGuard dg(cv.device);   // the caller's current device is restored on return
+  int rc = dg.err == hipSuccess ? BE_OK : pol_hip_fail(ctx, dg.err);
   hipError_t e = hipSuccess;
   if (rc == BE_OK) e = hipMalloc(&pol->img, (size_t)pol->L.total);
   if (rc == BE_OK && e == hipSuccess) e = hipMemset(pol->img, 0, (size_t)pol->L.total);
@@ -330,6 +325,7 @@ int be_policy_create(be_ctx* ctx, int32_t hidden, int32_t num_actions, be_policy
 
 int be_policy_destroy(be_policy* pol) {
   if (!pol) return BE_OK;
+  const DeviceGuard dg(pol->cv.device);   // the caller's current device is restored on return
   if (pol->img) (void)hipFree(pol->img);
   if (pol->obs4) (void)hipFree(pol->obs4);
   if (pol->zero4) (void)hipFree(pol->zero4);
@@ -343,7 +339,8 @@ int be_policy_load(be_policy* pol, const float* fc1_w, const float* fc1_b, const
   be_ctx* ctx = pol->ctx;
   if (!fc1_w || !fc1_b || !act_w || !act_b || !val_w || !val_b)
     return be_ctx_fail(ctx, BE_E_INVALID, "be_policy_load: a weight pointer is NULL");
-  if (int rc = pol_set_device(ctx, pol->cv.device)) return rc;
+  const DeviceGuard dg(pol->cv.device);   // the caller's current device is restored on return
+  POL_TRY(ctx, dg.err);
   const PolPack a{fc1_w, fc1_b, act_w, act_b, val_w, val_b, pol->H, pol->F, pol->A};
   hipLaunchKernelGGL(policy_pack_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a, pol->img, pol->L);
   POL_TRY(ctx, hipGetLastError());
@@ -366,7 +363,8 @@ int be_policy_act(be_policy* pol, const be_state* st, const uint8_t* obs, const 
   if (!pol->loaded) return be_ctx_fail(ctx, BE_E_INVALID, "be_policy_act before be_policy_load");
   if (!st || !st->episode || !st->ep_len || !obs || !out || !out->action)
     return be_ctx_fail(ctx, BE_E_INVALID, "be_policy_act needs state episode/ep_len, obs and out->action");
-  if (int rc = pol_set_device(ctx, pol->cv.device)) return rc;
+  const DeviceGuard dg(pol->cv.device);   // the caller's current device is restored on return
+  POL_TRY(ctx, dg.err);
   PParams p;
   memset(&p, 0, sizeof p);
   p.img = pol->img; p.obs = obs; p.episode = st->episode; p.ep_len = st->ep_len;
@@ -395,7 +393,8 @@ int be_policy_rollout(be_policy* pol, const be_state* st, const uint8_t* obs_in,
     return be_ctx_fail(ctx, BE_E_INVALID,
                        "be_policy_rollout needs 16-byte aligned obs buffers and num_envs * (4+W*W) % 16 == 0");
   if (steps == 0) return BE_OK;
-  if (int rc = pol_set_device(ctx, pol->cv.device)) return rc;
+  const DeviceGuard dg(pol->cv.device);   // the caller's current device is restored on return
+  POL_TRY(ctx, dg.err);
   const be_pol_rollout_args r{pol->img, pol->L.total, pol->k.HT, pol->k.KS, pol->k.NO, pol->A,
                               (unsigned long long)seed, obs_in, obs_last, steps, out, act};
   const int rc = be_internal_policy_rollout(ctx, st, &r, stream);

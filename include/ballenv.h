@@ -28,7 +28,10 @@
  *   - Layout is struct-of-arrays with the env index as the unit-stride axis:
  *     an (x, y) position is two int16 in one 32-bit word (x low, y high),
  *     i.e. an (N, 2) int16 array; per-obstacle arrays are (K, N, 2) int16.
- *   - One context per (device, config).  No internal threads.
+ *   - One context per (device, config).  No internal threads.  Every entry point
+ *     makes the context's device current for the call and restores the calling
+ *     thread's current device before it returns: no be_* call changes which GPU
+ *     the caller's later HIP / torch calls use.
  *   - Randomness (perf mode): Philox4x32-10 keyed by cfg.seed with counter
  *     (global env id, episode, ep_len, purpose|sub).  Every draw is a pure
  *     function of per-env state, so results do not depend on launch order,
@@ -64,7 +67,12 @@ enum {
   BE_STATUS_RESET_TAPE_EXHAUSTED = 1,  /* a reset consumed more draws than its tape held */
   BE_STATUS_REJECTION_LIMIT = 2,       /* a reset rejection loop hit its bound */
   BE_STATUS_BAD_ACTION = 4,            /* action index >= num_actions */
-  BE_STATUS_COORD_RANGE = 8,           /* a dynamic obstacle left the int16 range */
+  BE_STATUS_COORD_RANGE = 8,           /* a dynamic obstacle left the int16 range; the stored
+                                          coordinate wraps (two's complement int16).  The
+                                          reference's obstacles are unbounded ints (ballenv_env.py
+                                          :334-347).  be_config_check rejects configs that can get
+                                          here within an episode (autoreset with a time limit);
+                                          with time_limit 0 or autoreset 0 poll be_status. */
   BE_STATUS_NO_GOAL = 16               /* goal change with no other goal (reference raises) */
 };
 
@@ -143,7 +151,11 @@ typedef struct be_ctx be_ctx;
 int be_abi_version(void);
 /* Fill cfg with the ball_cnn_ac3.py / BallEnv defaults for N envs and window W. */
 int be_config_default(be_config* cfg, int32_t num_envs, int32_t window);
-/* Validate cfg; on failure returns BE_E_INVALID and writes a message into msg. */
+/* Validate cfg; on failure returns BE_E_INVALID and writes a message into msg.
+ * Besides the ranges, with autoreset and time_limit > 0 it requires
+ *   max spawn extent + max|obstacle_speed| * time_limit <= 32767
+ * (spawn extent: max(|strip_obs|, |screen - strip_obs|) per axis), so no dynamic obstacle can
+ * leave the int16 coordinates within an episode (BE_STATUS_COORD_RANGE).                    */
 int be_config_check(const be_config* cfg, char* msg, int32_t msg_len);
 /* Bytes of HBM traffic per env-step the step kernel is designed to move (u8 obs). */
 int64_t be_step_bytes(const be_config* cfg);
@@ -220,9 +232,9 @@ int be_status(be_ctx* ctx, int32_t* status_out, void* stream);
  * bytes, in device or host memory: a 64-byte header (magic "BALLENV1", ABI version, N, Ns, Nd,
  * blob bytes) then agent, goal, prev_dist, total_dist, ep_return, ep_len, episode, static_obs,
  * dyn_obs, dyn_goal in be_state order, each array at a 16-byte aligned offset.
- * be_save_state: asynchronous copies on the stream.  be_load_state: synchronises the stream to
- * check the header (BE_E_INVALID when it does not match this context's N / Ns / Nd), then copies
- * asynchronously.  A saved blob restores the envs bit for bit, Philox positions included
+ * be_save_state: asynchronous copies on the stream (graph-capturable).  be_load_state:
+ * SYNCHRONISES the stream to read and check the header (BE_E_INVALID when it does not match this
+ * context's N / Ns / Nd), then copies asynchronously -- it cannot be captured in a HIP graph.  A saved blob restores the envs bit for bit, Philox positions included
  * (episode / ep_len key every draw).                                                        */
 int64_t be_state_blob_bytes(const be_config* cfg);
 int be_save_state(be_ctx* ctx, const be_state* st, void* blob, void* stream);

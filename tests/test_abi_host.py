@@ -83,6 +83,28 @@ def test_config_check_rejects(field, value, msg):
     assert msg in _abi.config_check(c)
 
 
+def test_config_check_int16_coordinate_bound():
+    """int16 obstacle coordinates (the reference's are unbounded ints, ballenv_env.py:334-347):
+    with autoreset and a time limit, spawn extent + max|speed| * time_limit must stay <= 32767;
+    without that bound (time_limit 0 / autoreset 0) the config is accepted and the kernels flag
+    BE_STATUS_COORD_RANGE instead (tests/test_gpu_coord_range.py)."""
+    c = _abi.default_config(16, 10)
+    assert _abi.config_check(c) == ""                        # 500 + 1 * 1000
+    c.obstacle_speed[3] = -32                                # 500 + 32 * 1000 = 32500: still inside
+    assert _abi.config_check(c) == ""
+    c.obstacle_speed[3] = 33                                 # 33500
+    assert "int16 coordinate range" in _abi.config_check(c)
+    c.time_limit = 0                                         # unbounded episodes: allowed, status() polled
+    assert _abi.config_check(c) == ""
+    c.time_limit, c.autoreset = 1000, 0                      # a caller may step past done: allowed
+    assert _abi.config_check(c) == ""
+    c.autoreset, c.obstacle_speed[3] = 1, 1
+    c.strip_obs_x = -32000                                   # spawn x in [-32000, 32500): extent 32500
+    assert "int16 coordinate range" in _abi.config_check(c)
+    c.num_dynamic = 0                                        # no dynamic obstacles: nothing moves
+    assert _abi.config_check(c) == ""
+
+
 def test_config_needs_goal_per_dynamic_obstacle():
     c = EnvConfig(num_dynamic=6, obstacle_speed=[1] * 6)
     with pytest.raises(ValueError, match="goal per dynamic"):

@@ -36,7 +36,7 @@ def test_bench_json_line(gpu):
     cmd = [sys.executable, "bench.py", "--steps", "20", "--warmup", "5", "--settle", "60", "--no-cpu-baseline",
            "--policy-steps", "20", "--torch-policy-steps", "5", "--board-steps", "20", "--rollout-steps", "100",
            "--config2-steps", "50", "--config4-steps", "20", "--large-steps", "20", "--from-reset-steps", "20",
-           "--blocks-launches", "8"]
+           "--blocks-launches", "8", "--eager-steps", "50", "--shard-steps", "20"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -63,6 +63,80 @@ def test_bench_json_line(gpu):
             leg = d["blocks_obs"][f"envs_{n}"][kind]
             assert leg["value"] > 0 and leg["bytes_per_env"] == 8 + 4 * 18 + rowb and leg["roofline"]["frac"] > 0
     assert "cpu_baseline" not in d or d["cpu_baseline"] is None
+    # config 4's per-rank shards (the 1 -> 8 GPU prediction) and the eager drop-in leg
+    sh = c4["shards"]["by_gpus"]
+    assert [r["gpus"] for r in sh] == [2, 4, 8] and [r["envs_per_rank"] for r in sh] == [131072, 65536, 32768]
+    assert [r["env_offset"] for r in sh] == [131072, 196608, 229376]
+    for r in sh:
+        assert r["kernel_us_mean"] > 0 and r["projected_node_env_steps_per_s"] > 0 and 0 < r["moved_frac"] <= 1
+    eg = d["eager_step"]
+    assert eg["value"] > 0 and eg["host_us_per_step_call"] > 0 and eg["gpu_us_per_iteration"] > 0 and eg["steps"] == 50
+    check_bench_sources(d)
+
+
+def _walk(x, path=""):
+    if isinstance(x, dict):
+        yield path, x
+        for k, v in x.items():
+            yield from _walk(v, f"{path}.{k}")
+    elif isinstance(x, list):
+        for i, v in enumerate(x):
+            yield from _walk(v, f"{path}[{i}]")
+
+
+def check_bench_sources(d):
+    """Every roofline-bearing leg reports moved_frac <= 1 (the bytes actually moved: PMC, else the
+    engine's be_step_bytes); a frac above 1 (SURVEY's 390-B figure) carries frac_note; and every
+    committed profile a leg cites is the NEWEST round's file of that name for that kernel and size."""
+    import glob
+    import re
+    want = ["roofline", "config2.roofline", "config4.roofline", "large_batch.roofline", "from_reset.roofline",
+            "cold_action_rows", "fused_rollout", "board_profile.roofline", "board_profile.fused.roofline",
+            "policy_rollout.roofline", "blocks_obs.envs_65536.u8.roofline"]
+    seen = {p.lstrip("."): x for p, x in _walk(d)}
+    for w in want:
+        assert w in seen and "moved_frac" in seen[w], w
+    for p, x in seen.items():
+        if "moved_frac" in x:
+            assert 0 < x["moved_frac"] <= 1.0, (p, x["moved_frac"])
+        if (x.get("frac") or 0) > 1.0 and "bound" in x:
+            assert "frac_note" in x, p
+        for k, v in x.items():
+            if not (k.endswith("_source") and isinstance(v, str) and v.startswith("committed profile ")):
+                continue
+            rel = v[len("committed profile "):]
+            m = re.match(r"profiles/r(\d\d)_(.+)$", rel)
+            assert m, (p, k, v)
+            named = json.load(open(os.path.join(ROOT, rel)))
+            kern, units = named.get("kernel"), named.get("units_per_dispatch", named.get("envs"))
+            for other in glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_" + m.group(2))):
+                rnd = int(os.path.basename(other)[1:3])
+                if rnd > int(m.group(1)):
+                    o = json.load(open(other))
+                    assert not (o.get("kernel") == kern and o.get("units_per_dispatch", o.get("envs")) == units), \
+                        (p, k, v, "newer:", other)
+
+
+def test_bench_source_check_on_the_committed_line():
+    """check_bench_sources on the round's committed bench line, where one exists (CPU only)."""
+    lines = sorted(glob_bench_lines())
+    if not lines:
+        pytest.skip("no committed bench line with the moved_frac fields yet")
+    d = json.load(open(lines[-1]))
+    check_bench_sources(d)
+
+
+def glob_bench_lines():
+    import glob
+    out = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench.json")):
+        try:
+            d = json.load(open(f))
+        except ValueError:
+            continue
+        if isinstance(d, dict) and "moved_frac" in (d.get("roofline") or {}):
+            out.append(f)
+    return out
 
 
 _ONLY_HEADLINE = ["--no-cpu-baseline", "--policy-steps", "0", "--board-steps", "0", "--rollout-steps", "0",
