@@ -1027,9 +1027,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     for (int j = 0; j < NDC; ++j) { dp[j] = ld_s(p.dyn_obs + (size_t)j * N, ic); dgi[j] = ld_s(p.dyn_goal + (size_t)j * N, ic); }
 #pragma unroll
     for (int j = 0; j < NSC; ++j) so[j] = ld_s(p.static_obs + (size_t)j * N, ic);
-    old_dist = p.prev_read ? ld_s(p.prev_dist, ic) : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
+    // prev_dist read even when prev_read = 0 recomputes it, the select after every load is issued
+    // (a branch among the loads made the compiler wait for the agent / goal loads first)
+    const double old_read = ld_s(p.prev_dist, ic);
     total = ld_s(p.total_dist, ic);
     ret = ld_s(p.ep_return, ic);
+    __builtin_amdgcn_sched_barrier(0);
+    old_dist = p.prev_read ? old_read : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
   } else {
   tword[0] = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
   if (valid) {
@@ -1641,8 +1645,11 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   }
 #pragma unroll
   for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
-  // state[2] of the last step (prev_read = 0: recomputed, it is calc_dist(goal, agent) -- see KParams)
-  const double old_dist = p.prev_read ? ld_s(p.prev_dist, ic) : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
+  // state[2] of the last step, read even when prev_read = 0 recomputes it (calc_dist(goal, agent),
+  // see KParams) and the select after the scheduling barrier below: a branch among the loads made
+  // the compiler wait for the goal load (a register reused for a later address) before it issued
+  // total_dist, ep_return, the action and the stats slot -- the action a memory latency late
+  const double old_read = ld_s(p.prev_dist, ic);
   const double total = ld_s(p.total_dist, ic);
   double ret = ld_s(p.ep_return, ic);
   // the action last: the obstacle draws and moves below need no action, so a row that misses the
@@ -1658,6 +1665,8 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     sp1 = reinterpret_cast<const double2*>(slot)[1];
     sp2 = reinterpret_cast<const double2*>(slot)[2];
   }
+  __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any of them is used
+  const double old_dist = p.prev_read ? old_read : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
 #pragma unroll
   for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tt0 + j * TB, TW - 1)] = tword[j];
   // this wave's copy of the tables staged (state loads retire in order as used): a wave barrier, no
