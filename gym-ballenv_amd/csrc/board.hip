@@ -579,12 +579,6 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   // fused 2.96-3.05 against 3.05-3.08: profiles/r04_board_wave_actions_ab.txt)
   __shared__ double s_act_w[4][2 * BE_BOARD_MAX_ACTIONS];
   double* s_act = &s_act_w[w][0];
-  if (p.mode != 1 && p.actions) {   // (uniform)
-    if (lane < 2 * p.num_actions) s_act[lane] = (&p.tables->actions[0][0])[lane];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
   int a_pf = 0;
   double dx_pf = 0.0, dy_pf = 0.0;
   auto fetch = [&](int s) {
@@ -592,12 +586,24 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     if (p.actions) a_pf = p.actions[r];
     else { dx_pf = p.deltas[2 * r]; dy_pf = p.deltas[2 * r + 1]; }
   };
-  if (p.mode != 1) {
-    fetch(0);
-    // step 0's action lands before the loop: inside it the only pending read of a_pf is the one
-    // issued a step earlier, so its wait need not cover that step's stores (vmcnt(#stores), where a
-    // loop entered with a_pf in flight merges to vmcnt(0))
-    if constexpr (ROLL) asm volatile("" ::"v"(a_pf), "v"(dx_pf), "v"(dy_pf));
+  // the table word (a clamped index: no branch around the load), then step 0's action, then the
+  // LDS write: the write waits for the table word only, not for the action -- written the other way
+  // round the action load was issued after that wait, a second memory latency in the prologue
+  const bool stage_act = p.mode != 1 && p.actions;   // (uniform)
+  double tword = 0.0;
+  if (stage_act) tword = (&p.tables->actions[0][0])[min(lane, 2 * BE_BOARD_MAX_ACTIONS - 1)];
+  if (p.mode != 1) fetch(0);
+  if (stage_act) {
+    if (lane < 2 * p.num_actions) s_act[lane] = tword;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // step 0's action lands before the loop: inside it the only pending read of a_pf is the one
+  // issued a step earlier, so its wait need not cover that step's stores (vmcnt(#stores), where a
+  // loop entered with a_pf in flight merges to vmcnt(0))
+  if constexpr (ROLL) {
+    if (p.mode != 1) asm volatile("" ::"v"(a_pf), "v"(dx_pf), "v"(dy_pf));
   }
   for (int s = 0; s < steps; ++s) {
     const int64_t row = (int64_t)s * p.n + i;   // this step's output row (i for modes 0 / 1)

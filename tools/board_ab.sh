@@ -4,8 +4,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/board_ab
-ARGS="--no-cpu-baseline --steps 10 --warmup 2 --policy-steps 0 --rollout-steps 0 --board-steps 1000 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0"
-for r in 1 2; do
+ARGS="--no-cpu-baseline --steps 10 --warmup 2 --policy-steps 0 --rollout-steps 0 --board-steps 1000 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0 --config4-steps 0 --shard-steps 0 --eager-steps 0"
+for r in $(seq 1 ${REPS:-2}); do
   for v in new ${B:-boardold}; do   # B: one or more A/B builds under tools/diag
     if [ $v = new ]; then L=""; else L=tools/diag/$v/libballenv.so; fi
     BALLENV_LIB=$L timeout -k 10 200 python3 bench.py $ARGS > gpurun_out/board_ab/$v.$r.log 2>&1
