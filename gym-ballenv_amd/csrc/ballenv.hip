@@ -1645,11 +1645,12 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   }
 #pragma unroll
   for (int j = 0; j < SS; ++j) so[j] = ld_s(p.static_obs, (uint32_t)min(L * j + h, NSC - 1) * (uint32_t)N + ic);
-  // state[2] of the last step, read even when prev_read = 0 recomputes it (calc_dist(goal, agent),
-  // see KParams) and the select after the scheduling barrier below: a branch among the loads made
-  // the compiler wait for the goal load (a register reused for a later address) before it issued
-  // total_dist, ep_return, the action and the stats slot -- the action a memory latency late
-  const double old_read = ld_s(p.prev_dist, ic);
+  // state[2] of the last step (prev_read = 0: recomputed, it is calc_dist(goal, agent) -- see KParams).
+  // (Read unconditionally with the select after a scheduling barrier, so that the action is issued
+  // with the other loads instead of after the goal load lands: 5.26-5.27 against 5.22-5.24 us at
+  // 32 768 envs, the same within noise at 65 536 -- profiles/r05_prologue_ab.txt, not kept here; it
+  // is kept in the one-lane kernel, 8.05 against 8.13-8.15 us at 131 072)
+  const double old_dist = p.prev_read ? ld_s(p.prev_dist, ic) : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
   const double total = ld_s(p.total_dist, ic);
   double ret = ld_s(p.ep_return, ic);
   // the action last: the obstacle draws and moves below need no action, so a row that misses the
@@ -1665,8 +1666,6 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     sp1 = reinterpret_cast<const double2*>(slot)[1];
     sp2 = reinterpret_cast<const double2*>(slot)[2];
   }
-  __builtin_amdgcn_sched_barrier(0);   // every load above is issued before any of them is used
-  const double old_dist = p.prev_read ? old_read : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
 #pragma unroll
   for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tt0 + j * TB, TW - 1)] = tword[j];
   // this wave's copy of the tables staged (state loads retire in order as used): a wave barrier, no
@@ -1688,7 +1687,8 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   if (counter < 0) counter += p.goal_change + 1;
   if (counter > p.goal_change) counter -= p.goal_change + 1;
   const bool change = counter >= p.goal_change;
-  const u4 b0 = philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
+  const u4 b0 = DBG(DBG_NO_PHILOX) ? u4{gid, episode, (uint32_t)len0, gid ^ episode}   // (ablation: wrong draws)
+                                   : philox(gid, episode, (uint32_t)len0, tag(PURPOSE_STEP_OBS, 0u), p.seed);
   DIAG(7);
   uint32_t st_flags = 0u;
   int ngs[SD];

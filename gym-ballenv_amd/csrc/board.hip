@@ -586,24 +586,38 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
     if (p.actions) a_pf = p.actions[r];
     else { dx_pf = p.deltas[2 * r]; dy_pf = p.deltas[2 * r + 1]; }
   };
-  // the table word (a clamped index: no branch around the load), then step 0's action, then the
-  // LDS write: the write waits for the table word only, not for the action -- written the other way
-  // round the action load was issued after that wait, a second memory latency in the prologue
   const bool stage_act = p.mode != 1 && p.actions;   // (uniform)
-  double tword = 0.0;
-  if (stage_act) tword = (&p.tables->actions[0][0])[min(lane, 2 * BE_BOARD_MAX_ACTIONS - 1)];
-  if (p.mode != 1) fetch(0);
-  if (stage_act) {
-    if (lane < 2 * p.num_actions) s_act[lane] = tword;
+  auto act_barrier = [] {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  // step 0's action lands before the loop: inside it the only pending read of a_pf is the one
-  // issued a step earlier, so its wait need not cover that step's stores (vmcnt(#stores), where a
-  // loop entered with a_pf in flight merges to vmcnt(0))
-  if constexpr (ROLL) {
-    if (p.mode != 1) asm volatile("" ::"v"(a_pf), "v"(dx_pf), "v"(dy_pf));
+  };
+  if constexpr (!ROLL) {
+    // the per-step kernel: the table word (a clamped index: no branch around the load), then step
+    // 0's action, then the LDS write, which waits for the table word only -- the other way round the
+    // action load was issued after that wait, a second memory latency in the prologue (step
+    // 8.06-8.10 -> 7.89-7.91 us, profiles/r05_board_prologue_ab.txt)
+    double tword = 0.0;
+    if (stage_act) tword = (&p.tables->actions[0][0])[min(lane, 2 * BE_BOARD_MAX_ACTIONS - 1)];
+    if (p.mode != 1) fetch(0);
+    if (stage_act) {
+      if (lane < 2 * p.num_actions) s_act[lane] = tword;
+      act_barrier();
+    }
+  } else {
+    // the fused kernel keeps the table first: its prologue is once per launch, and the per-step
+    // kernel's order cost its loop 0.25 us per step (the same A/B)
+    if (stage_act) {
+      if (lane < 2 * p.num_actions) s_act[lane] = (&p.tables->actions[0][0])[lane];
+      act_barrier();
+    }
+    if (p.mode != 1) {
+      fetch(0);
+      // step 0's action lands before the loop: inside it the only pending read of a_pf is the one
+      // issued a step earlier, so its wait need not cover that step's stores (vmcnt(#stores), where a
+      // loop entered with a_pf in flight merges to vmcnt(0))
+      asm volatile("" ::"v"(a_pf), "v"(dx_pf), "v"(dy_pf));
+    }
   }
   for (int s = 0; s < steps; ++s) {
     const int64_t row = (int64_t)s * p.n + i;   // this step's output row (i for modes 0 / 1)

@@ -96,3 +96,42 @@ def test_graph_replayed_board_steps_equal_eager(gpu):
     assert n_done > 0
     for b in (eager, graphed):
         b.close()
+
+
+def test_graph_captured_batched_step_api(gpu):
+    """BatchedBallEnv.step() itself inside torch.cuda.graph: the caller's
+    loop -- one torch op writing the actions into a fixed buffer, then env.step(buffer) -- captured
+    and replayed equals the same loop run eagerly (step() is asynchronous on the current stream, uses
+    the caller's stream handle and allocates nothing on its fast path)."""
+    from gym_ballenv_amd.config import EnvConfig
+    N, W, T = 32768, 10, 40
+    cfg_py = EnvConfig(time_limit=25)
+    eager, graphed = (make_env(cfg_py, N, W, gpu, seed=77) for _ in range(2))
+    acts = eager.sample_actions(T, seed=9)
+    for e in (eager, graphed):
+        e.reset()
+    buf = torch.empty(N, dtype=torch.uint8, device=gpu)
+    graphed.step(buf.copy_(acts[0]))          # first call (checks) outside the capture; replayed below too
+    rec = torch.empty((T, N, graphed.obs_dim), dtype=torch.uint8, device=gpu)
+    rew = torch.empty((T, N), dtype=torch.float64, device=gpu)
+    side = torch.cuda.Stream(gpu)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        for t in range(1, T):
+            buf.copy_(acts[t])
+            obs, reward, done, info = graphed.step(buf)
+            rec[t].copy_(obs)
+            rew[t].copy_(reward)
+    g.replay()
+    torch.cuda.synchronize(gpu)
+    for t in range(T):
+        obs, reward, done, info = eager.step(acts[t])
+        if t:
+            assert torch.equal(rec[t], obs), f"obs t={t}"
+            assert torch.equal(rew[t], reward), f"reward t={t}"
+    a, b = np_state(eager), np_state(graphed)
+    for k in KEYS:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    for e in (eager, graphed):
+        e.status()
+        e.close()

@@ -38,6 +38,7 @@ def make(n, autoreset, tl, spread):
     for _ in range(3):
         g.replay()
     torch.cuda.synchronize()
+    env._keep_acts = acts      # the graph reads these rows: keep them alive
     return env, g
 
 
