@@ -77,6 +77,19 @@ struct Tables {
   uint8_t hw[HW_MAX + 1];                     // floor(sqrt(R^2 - d^2)), d = 0..R (only when R <= HW_MAX)
 };
 
+// step2_kernel's 64-bit row-span table (W = 10, W-1+2R <= 63): span[j] holds the cells an obstacle
+// at window column C = W-1+R lights in a row at distance |j - J0| (J0 = R+K-1): bits C-hw .. C+hw,
+// 0 past R.  A near entry at window (f, e) lights row k with span[e - k + J0] >> (C - f), clipped to
+// W bits -- one LDS read, one shift and one OR per row (raster_rows_span).  It follows Tables in the
+// same device buffer; only step2_kernel stages it.
+constexpr int SPAN_N = 72;
+struct TablesX {
+  Tables t;
+  uint64_t span[SPAN_N];
+};
+static_assert(sizeof(Tables) % 16 == 0 && sizeof(TablesX) % 16 == 0, "16-byte table staging");
+__host__ __device__ constexpr bool span_fits(int W, int R) { return W == 10 && W - 1 + 2 * R <= 63 && 2 * R + 2 * (W - 1) - 1 <= SPAN_N; }
+
 // Kernel arguments: hot fields first, 64-byte lines (see the latency notes above).
 struct KParams {
   // line 0
@@ -340,6 +353,26 @@ __device__ __forceinline__ void raster_rows_mt(const NearList<BLOCK>& nl, int R,
 #pragma unroll
     for (int k = 0; k < K; ++k) rows[k] |= col[min(abs(e - k), R + 1)];
   }
+}
+
+// raster_rows<WT, BLOCK, true> from the 64-bit span table (TablesX; span_fits(WT, R)), bit for bit:
+// an entry's rows cost one LDS read, one 64-bit shift and one OR each instead of the span arithmetic.
+template <int WT, int BLOCK>
+__device__ __forceinline__ void raster_rows_span(const NearList<BLOCK>& nl, int R, uint32_t (&rows)[Geo<WT>::K],
+                                                 const uint64_t* span) {
+  constexpr int K = Geo<WT>::K;
+#pragma unroll
+  for (int k = 0; k < K; ++k) rows[k] = 0u;
+  for (int n = 0; n < nl.cnt; ++n) {
+    int f, e;
+    nl.get(n, f, e);                                   // agent-relative: window (f + W/2, e + W/2)
+    const uint64_t* col = span + (e + WT / 2 + R);    // row k: span[e + W/2 - k + J0] = col[K-1-k]
+    const uint32_t sh = (uint32_t)(WT - 1 + R - (f + WT / 2));   // C - f, in [0, W-1+2R] for a near entry
+#pragma unroll
+    for (int k = 0; k < K; ++k) rows[k] |= (uint32_t)(col[K - 1 - k] >> sh);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) rows[k] &= (1u << WT) - 1u;
 }
 
 // Flatten rows into prep_state4's cell order (window row r uses distinct row max(r-1,0): quirk Q1).
@@ -1587,6 +1620,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
 //    the count re-reads a real obstacle and is masked out), moves / tests / stores them and
 //    keeps its own near list;
 //  * the pair's collision flags and window rows are OR-ed with one DPP op each;
+//  * a near entry's rows come from the wave's copy of the 64-bit span table (raster_rows_span:
+//    a read, a shift and an OR per row; 6.18 against 6.39 us at 65 536 envs, 5.09 against 5.24 at
+//    32 768 -- profiles/r05_step2_span_raster_ab.txt), so pick_kernel takes this kernel only while
+//    W-1+2R <= 63 (R <= 27; the defaults' R is 25), the one-lane kernel past it;
 //  * lane h writes its half of the obs row (uint2 words [7h, 7h+7)) into the wave's stage and
 //    half of the per-env scalar stores (a per-lane pointer select: one store instruction);
 //  * the Philox block, the agent move, the f64 reward and done run on both lanes (the same
@@ -1608,9 +1645,9 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   static_assert(NDC <= 5, "one Philox block of 24-bit fields");
   static_assert(16 * KR >= (64 / (NSC + NDC)) * (KR + 4), "wave reset scratch");
   extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ Tables t_wave[NWAVE];               // one copy of the tables per wave (no block barrier)
+  __shared__ __align__(16) TablesX t_wave[NWAVE];   // one copy of the tables per wave (no block barrier)
   __shared__ uint32_t s_rows[NWAVE][16 * KR];    // wave_resets scratch (row masks + stash)
-  constexpr int TW = (int)(sizeof(Tables) / 4);
+  constexpr int TW = (int)(sizeof(TablesX) / 16);   // 16-byte table words
 
   DIAG(0);
   if (DBG(DBG_EXIT_ENTRY)) return;
@@ -1620,7 +1657,8 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   const bool valid = i < N;
   const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
   NearList<CT> nl{reinterpret_cast<uint32_t*>(smem) + tid, 0};
-  Tables& t = t_wave[w];
+  Tables& t = t_wave[w].t;
+  const uint64_t* span = t_wave[w].span;
   uint8_t* stage = stage_blk + (size_t)w * EPW * F;   // the wave's 32 rows
   constexpr int TB = 64;     // each wave stages its own copy of the tables
   const int tt0 = lane;
@@ -1628,10 +1666,10 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   // ---- every load, straight-line, in use order (32-bit element offsets from uniform bases;
   //      obstacle k of lane h at element k*N + env: pick_kernel keeps NS*N < 2^30)
   constexpr int TL = (TW + TB - 1) / TB;   // table words per lane (each wave stages its own copy)
-  uint32_t tword[TL];
+  uint4 tword[TL];
 #pragma unroll
   for (int j = 0; j < TL; ++j)
-    tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min(tt0 + j * TB, TW - 1));
+    tword[j] = ld_s(reinterpret_cast<const uint4*>(p.tables), (uint32_t)min(tt0 + j * TB, TW - 1));
   const uint32_t episode = ld_s(p.episode, ic);
   const int len0 = ld_s(p.ep_len, ic);
   const int32_t agent0 = ld_s(p.agent, ic), goal0 = ld_s(p.goal, ic);
@@ -1667,7 +1705,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     sp2 = reinterpret_cast<const double2*>(slot)[2];
   }
 #pragma unroll
-  for (int j = 0; j < TL; ++j) reinterpret_cast<uint32_t*>(&t)[min(tt0 + j * TB, TW - 1)] = tword[j];
+  for (int j = 0; j < TL; ++j) reinterpret_cast<uint4*>(&t_wave[w])[min(tt0 + j * TB, TW - 1)] = tword[j];
   // this wave's copy of the tables staged (state loads retire in order as used): a wave barrier, no
   // block barrier in the kernel -- 6.38-6.40 against 6.45-6.46 us with one block copy under a block
   // barrier (profiles/r04_step2_wave_tables_ab.txt; round 2 had measured the two the same)
@@ -1789,7 +1827,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   for (int k = 0; k < KR; ++k) xrows[k] = 0u;
   if (do_reset && p.terminal_obs) {   // both lanes of the pair take this branch together
     uint32_t rows[KR], flat[NW];
-    raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
+    raster_rows_span<WT, CT>(nl, p.R, rows, span);
 #pragma unroll
     for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k]);
     flatten<WT>(rows, flat);
@@ -1835,7 +1873,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   // ---- observation (prep_state4): own near list -> rows, OR-ed over the pair, half a row each
   {
     uint32_t rows[KR], flat[NW];
-    raster_rows<WT, CT, true>(nl, g0, rows, t.hw);
+    raster_rows_span<WT, CT>(nl, p.R, rows, span);
 #pragma unroll
     for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k] | xrows[k]);
     flatten<WT>(rows, flat);
@@ -2964,7 +3002,8 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lane
   bool staged = true;
   const bool fixed = fixed_ok && mode == MODE_STEP && c.num_static == FIX_NS && c.num_dynamic == FIX_ND &&
                      c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
-  if (fixed && lanes10 == 2 && W == 10 && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
+  if (fixed && lanes10 == 2 && W == 10 && span_fits(W, c.radius_obstacle + c.radius_agent) &&
+      (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
     // two lanes per env (step2_kernel): 32 envs per wave, 128 per block
     L.fn = step2_kernel<10, FIX_NS, FIX_ND>;
     L.epb = S2_CT / 2;
@@ -3051,11 +3090,11 @@ Launch pick_policy_rollout(const be_config& c, bool fixed_ok, int HT, int KS, in
 // ====================================================================== C ABI
 struct be_ctx {
   be_config cfg;
-  Tables tables;
+  TablesX tables;
   KParams base;      // config-derived part of every launch's KParams
   int device;
   int* status;
-  Tables* d_tables;
+  TablesX* d_tables;
   bool generic_only;   // BALLENV_GENERIC_KERNELS=1: never use the fixed-shape step kernels (A/B diagnostics)
   bool unit_moves;     // every action move in {-1,0,1}^2 (fixed-shape kernels' packed table)
   bool distinct_goals; // >= 2 pairwise-distinct goals (fixed-shape kernels' arithmetic newGoalList)
@@ -3330,8 +3369,8 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   if (hipDeviceGetAttribute(&ctx->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess ||
       ctx->max_lds <= 0)
     ctx->max_lds = 65536;
-  Tables& t = ctx->tables;
-  memset(&t, 0, sizeof t);
+  memset(&ctx->tables, 0, sizeof ctx->tables);
+  Tables& t = ctx->tables.t;
   for (int k = 0; k < cfg->num_dynamic; ++k) t.speed[k] = cfg->obstacle_speed[k];
   t.strip_obs_x = cfg->strip_obs_x; t.strip_obs_y = cfg->strip_obs_y;
   t.strip_goal_x = cfg->strip_goal_x; t.strip_goal_y = cfg->strip_goal_y;
@@ -3353,12 +3392,19 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
     while ((h + 1) * (h + 1) <= R * R - d * d) ++h;
     t.hw[d] = (uint8_t)h;
   }
+  if (span_fits(cfg->window, R)) {   // step2_kernel's row-span table (TablesX)
+    const int W = cfg->window, C = W - 1 + R, J0 = R + W - 2;
+    for (int j = 0; j < SPAN_N; ++j) {
+      const int a = abs(j - J0), hw = a <= R ? t.hw[a] : 0;
+      ctx->tables.span[j] = a <= R && j <= 2 * J0 ? ((2ull << (2 * hw)) - 1ull) << (C - hw) : 0ull;
+    }
+  }
   const DeviceGuard dg(device);   // the caller's current device is restored on return
   hipError_t e = dg.err;
   if (e == hipSuccess) e = hipMalloc(&ctx->status, sizeof(int));
   if (e == hipSuccess) e = hipMemset(ctx->status, 0, sizeof(int));
-  if (e == hipSuccess) e = hipMalloc(&ctx->d_tables, sizeof(Tables));
-  if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, &ctx->tables, sizeof(Tables), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&ctx->d_tables, sizeof(TablesX));
+  if (e == hipSuccess) e = hipMemcpy(ctx->d_tables, &ctx->tables, sizeof(TablesX), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   // be_step's two possible kernels, picked once (pick_kernel formats a name: not per launch)
   ctx->step_launch[0] = pick_kernel(ctx->cfg, MODE_STEP, false, ctx->step_lanes, ctx->step5_lpe);
@@ -3404,7 +3450,7 @@ static KParams make_params(be_ctx* ctx, const be_state* st, const be_out* out) {
     a.truncated = out->truncated; a.terminal_obs = out->terminal_obs; a.final_return = out->final_return;
     a.final_len = out->final_len; a.stats = out->stats;
   }
-  a.tables = ctx->d_tables;
+  a.tables = &ctx->d_tables->t;
   a.status = ctx->status;
   return a;
 }

@@ -398,6 +398,33 @@ def test_step2_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
         e.close()
 
 
+@pytest.mark.parametrize("r_obs", [22, 23])
+def test_step2_span_table_radius_bound(gpu, r_obs):
+    """step2_kernel rasterises from a 64-bit row-span table, which holds W-1+2R <= 63 (R <= 27 at
+    W=10; the default R is 25).  R = 27 (the widest table) is bit-exact against the oracle; at R = 28
+    the dispatch takes the one-lane fixed-shape kernel, also bit-exact."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig(radius_obstacle=r_obs, time_limit=40)
+    N, a, k, W = 8192, 4096, SLICE, 10
+    rng = np.random.default_rng(r_obs)
+    env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, k, seed=0x5A, rng=rng)
+    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5>" if r_obs + 5 <= 27 else "be_kernel<10, 0, 13, 5>")
+    acts = env.sample_actions(60, seed=0x5A)
+    lit = 0
+    for t in range(60):
+        out["terminal_obs"][:] = 0
+        env.terminal_obs.zero_()
+        oracle.step(cfg, st, out, actions=acts[t, a:a + k].cpu().numpy())
+        obs, reward, done, info = env.step(acts[t])
+        _check_step(t, a, k, out, obs, reward, done, info["truncated"], info["final_return"], info["final_len"],
+                    info["terminal_obs"])
+        _check_state(env, st, a, k, f"t={t}")
+        lit += int((out["obs"][:, 4:] != 0).any(1).sum())
+    assert lit > 0
+    env.status()
+    env.close()
+
+
 def test_step_n_equals_step_calls(gpu):
     """be_step_n (K launches queued by one call) leaves the same state, last-step outputs and
     stats slots as K be_step calls."""
