@@ -38,6 +38,7 @@
 // Everything is integer except the reward path, which is f64 with the same
 // operation order as the reference (correctly rounded sqrt/div, no FMA
 // contraction: built with -ffp-contract=off), so results are bit-exact.
+#include <type_traits>
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -77,18 +78,20 @@ struct Tables {
   uint8_t hw[HW_MAX + 1];                     // floor(sqrt(R^2 - d^2)), d = 0..R (only when R <= HW_MAX)
 };
 
-// step2_kernel's 64-bit row-span table (W = 10, W-1+2R <= 63): span[j] holds the cells an obstacle
+// The fixed-shape step kernels' 64-bit row-span table (span_fits: W-1+2R <= 63): span[j] holds the cells an obstacle
 // at window column C = W-1+R lights in a row at distance |j - J0| (J0 = R+K-1): bits C-hw .. C+hw,
 // 0 past R.  A near entry at window (f, e) lights row k with span[e - k + J0] >> (C - f), clipped to
 // W bits -- one LDS read, one shift and one OR per row (raster_rows_span).  It follows Tables in the
-// same device buffer; only step2_kernel stages it.
+// same device buffer; only the fixed-shape step kernels stage it.
 constexpr int SPAN_N = 72;
 struct TablesX {
   Tables t;
   uint64_t span[SPAN_N];
 };
 static_assert(sizeof(Tables) % 16 == 0 && sizeof(TablesX) % 16 == 0, "16-byte table staging");
-__host__ __device__ constexpr bool span_fits(int W, int R) { return W == 10 && W - 1 + 2 * R <= 63 && 2 * R + 2 * (W - 1) - 1 <= SPAN_N; }
+__host__ __device__ constexpr bool span_fits(int W, int R) {   // W >= 2: K = W-1 rows, J0 = R+W-2
+  return W >= 2 && R >= 0 && W - 1 + 2 * R <= 63 && 2 * R + 2 * (W - 1) - 1 <= SPAN_N;
+}
 
 // Kernel arguments: hot fields first, 64-byte lines (see the latency notes above).
 struct KParams {
@@ -972,6 +975,21 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
 // NSC/NDC > 0: a step kernel specialised for exactly NSC static / NDC dynamic obstacles in
 // Philox mode (no tape), one lane per env -- every obstacle loop is unrolled to its exact
 // trip count (the dispatcher picks it only for a matching config).
+__device__ __forceinline__ Tables& tab_of(TablesX& x) { return x.t; }
+__device__ __forceinline__ Tables& tab_of(Tables& x) { return x; }
+// be_kernel's rasteriser: FIXED from the wave's span table when it fits R (a uniform branch),
+// the half-width table otherwise; the generic kernels their span arithmetic.
+template <int WT, bool FIXED, class TT>
+__device__ __forceinline__ void raster_fixed(const NearList<BLOCK_THREADS>& nl, const Win& g, int R,
+                                             uint32_t (&rows)[Geo<WT>::K], TT& tb) {
+  if constexpr (FIXED) {
+    if (span_fits(WT, R)) raster_rows_span<WT, BLOCK_THREADS>(nl, R, rows, tb.span);
+    else raster_rows<WT, BLOCK_THREADS, true>(nl, g, rows, tb.t.hw);
+  } else {
+    raster_rows<WT, BLOCK_THREADS, false>(nl, g, rows, tab_of(tb).hw);
+  }
+}
+
 template <int WT, int MODE, int NSC = 0, int NDC = 0>
 __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   constexpr bool FIXED = NSC > 0 || NDC > 0;
@@ -985,7 +1003,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   // FIXED: one copy of the tables per wave, so the fixed-shape kernel has no block barrier (8.11-8.21
   // against 8.15-8.27 us at 131 072 envs, the same within noise at 262 144 and 2^20 envs:
   // profiles/r04_onelane_wave_tables_ab.txt)
-  __shared__ Tables t_blk[FIXED ? BLOCK_THREADS / 64 : 1];
+  // (FIXED: TablesX, the row-span table included)
+  __shared__ __align__(16) std::conditional_t<FIXED, TablesX, Tables> t_blk[FIXED ? BLOCK_THREADS / 64 : 1];
   // block-cooperative reset list and block stats: the generic kernels only.  FIXED never
   // initialises or reads them (it resets wave by wave through wave_resets and folds its stats per
   // half-wave), so they are sized 1 there: a FIXED change that needs them must size them again.
@@ -999,12 +1018,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   __shared__ uint32_t s_rows[RCAP][KR];            // FIXED too: 16 rows of wave_resets scratch per wave
   constexpr int TW = (int)(sizeof(Tables) / 4);
   static_assert(TW <= BLOCK_THREADS && sizeof(Tables) % 4 == 0, "table staging assumes <= 256 words");
+  constexpr int TW4 = (int)(sizeof(TablesX) / 16);   // FIXED: 16-byte words of TablesX per wave copy
 
   DIAG(0);
   if (DBG(DBG_EXIT_ENTRY)) return;
   const int N = p.n, Ns = FIXED ? NSC : p.ns, Nd = FIXED ? NDC : p.nd;
   const int tid = threadIdx.x;
-  Tables& t = t_blk[FIXED ? (tid >> 6) : 0];
+  Tables& t = tab_of(t_blk[FIXED ? (tid >> 6) : 0]);
   const int q = tid & (LPE - 1);                  // lane within the env's group
   const int el = tid / LPE;                        // env within the block
   const int blk0 = (int)blockIdx.x * EPB;
@@ -1038,10 +1058,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   for (int j = 0; j < SPL; ++j) so[j] = 0;
 #pragma unroll
   for (int j = 0; j < DPL; ++j) { dp[j] = 0; dgi[j] = 0; t0[j] = 0; t1[j] = 0; }
-  constexpr int TLW = FIXED ? (TW + 63) / 64 : 1;   // table words per lane
-  uint32_t tword[TLW];
+  constexpr int TLW = FIXED ? (TW4 + 63) / 64 : 1;   // table words per lane (FIXED: 16-byte)
+  uint4 tword[TLW];
 #pragma unroll
-  for (int j = 0; j < TLW; ++j) tword[j] = 0u;
+  for (int j = 0; j < TLW; ++j) tword[j] = uint4{0u, 0u, 0u, 0u};
   if constexpr (FIXED) {
     // straight-line prologue (no branches around loads, clamped env index; invalid lanes
     // never store): the waitcnt pass can then retire the loads one by one -- tables
@@ -1050,7 +1070,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     const uint32_t ic = (uint32_t)min(i, N - 1);
 #pragma unroll
     for (int j = 0; j < TLW; ++j)
-      tword[j] = ld_s(reinterpret_cast<const uint32_t*>(p.tables), (uint32_t)min((tid & 63) + j * 64, TW - 1));
+      tword[j] = ld_s(reinterpret_cast<const uint4*>(p.tables), (uint32_t)min((tid & 63) + j * 64, TW4 - 1));
     episode = ld_s(p.episode, ic);
     len0 = ld_s(p.ep_len, ic);
     a = ld_s(p.actions, ic);
@@ -1068,7 +1088,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     __builtin_amdgcn_sched_barrier(0);
     old_dist = p.prev_read ? old_read : calc_dist(px(goal0), py(goal0), px(agent0), py(agent0));
   } else {
-  tword[0] = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
+  tword[0].x = tid < TW ? reinterpret_cast<const uint32_t*>(p.tables)[tid] : 0u;
   if (valid) {
     // issue order = use order: vmcnt retires loads in order, so the Philox draws (keyed by
     // episode, ep_len) and the obstacle moves start while the statics and f64s are in flight
@@ -1103,12 +1123,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   }
   if constexpr (FIXED) {   // this wave's copy of the tables; nothing else is block-shared here
 #pragma unroll
-    for (int j = 0; j < TLW; ++j) reinterpret_cast<uint32_t*>(&t)[min((tid & 63) + j * 64, TW - 1)] = tword[j];
+    for (int j = 0; j < TLW; ++j) reinterpret_cast<uint4*>(&t_blk[tid >> 6])[min((tid & 63) + j * 64, TW4 - 1)] = tword[j];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   } else {
-    if (tid < TW) reinterpret_cast<uint32_t*>(&t)[tid] = tword[0];
+    if (tid < TW) reinterpret_cast<uint32_t*>(&t)[tid] = tword[0].x;
     if (EPB == BLOCK_THREADS || tid < EPB) s_slot_of[tid] = -1;
     if (tid == 0) s_nreset = 0;
     __syncthreads();  // barrier 1: tables staged (the state loads retire in order as they are used)
@@ -1328,7 +1348,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const int quad = quadrant(ax, ay, gx, gy);
       if constexpr (WT > 0) {
         uint32_t rows[Geo<WT>::K], flat[Geo<WT>::NW];
-        raster_rows<WT, BLOCK_THREADS, FIXED>(nl, g, rows, t.hw);
+        raster_fixed<WT, FIXED>(nl, g, p.R, rows, t_blk[FIXED ? (tid >> 6) : 0]);
 #pragma unroll
         for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k]);
         flatten<WT>(rows, flat);
@@ -1414,7 +1434,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const Win g(p, ax, ay);
       uint32_t rows[Geo<WT>::K];
       if (DBG(DBG_NO_RASTER)) nl.cnt = 0;
-      raster_rows<WT, BLOCK_THREADS, FIXED>(nl, g, rows, t.hw);
+      raster_fixed<WT, FIXED>(nl, g, p.R, rows, t_blk[FIXED ? (tid >> 6) : 0]);
 #pragma unroll
       for (int k = 0; k < Geo<WT>::K; ++k) rows[k] = group_or<LPE>(rows[k] | xrows[k]);
       flatten<WT>(rows, flat);
@@ -3393,7 +3413,7 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
     t.hw[d] = (uint8_t)h;
   }
   if (span_fits(cfg->window, R)) {   // step2_kernel's row-span table (TablesX)
-    const int W = cfg->window, C = W - 1 + R, J0 = R + W - 2;
+    const int W = cfg->window, C = W - 1 + R, J0 = R + W - 2;   // K = W-1 rows
     for (int j = 0; j < SPAN_N; ++j) {
       const int a = abs(j - J0), hw = a <= R ? t.hw[a] : 0;
       ctx->tables.span[j] = a <= R && j <= 2 * J0 ? ((2ull << (2 * hw)) - 1ull) << (C - hw) : 0ull;

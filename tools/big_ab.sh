@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/big_ab; mkdir -p $O
-ARGS="--no-cpu-baseline --steps 10 --warmup 2 --policy-steps 0 --torch-policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 0 --config4-steps 1000 --config4-envs ${ENVS4:-262144} --large-steps ${LARGE:-1000} --from-reset-steps 0 --blocks-launches 0"
+ARGS="--no-cpu-baseline --steps 10 --warmup 2 --policy-steps 0 --torch-policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 0 --config4-steps 1000 --config4-envs ${ENVS4:-262144} --large-steps ${LARGE:-1000} --from-reset-steps 0 --blocks-launches 0 --shard-steps 0 --eager-steps 0"
 for r in $(seq 1 ${REPS:-3}); do
   for v in new ${B}; do
     L=""; [ $v != new ] && L=tools/diag/$v/libballenv.so
