@@ -1650,6 +1650,18 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
 //    instruction stream, so no extra issue).
 // Autoreset is wave_resets with the even lanes as owners; stats fold per wave (32 envs =
 // one be_stats_slots slot) in env order, as be_kernel's half-wave folds do.
+// byte sel of x times k (24-bit), as one SDWA multiply: the compiler folds a byte select back into a
+// shift and a mask, which costs two more VALU per obs word
+__device__ __forceinline__ uint32_t mul24_byte(uint32_t x, uint32_t k, int sel) {
+  uint32_t r;
+  switch (sel) {
+    case 0: asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD" : "=v"(r) : "v"(x), "v"(k)); break;
+    case 1: asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(r) : "v"(x), "v"(k)); break;
+    case 2: asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "=v"(r) : "v"(x), "v"(k)); break;
+    default: asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(r) : "v"(x), "v"(k)); break;
+  }
+  return r;
+}
 __device__ __forceinline__ uint32_t pair_or(uint32_t x) {   // OR with the other lane of the pair
   return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
 }
@@ -1892,26 +1904,35 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
 
   // ---- observation (prep_state4): own near list -> rows, OR-ed over the pair, half a row each
   {
-    uint32_t rows[KR], flat[NW];
+    uint32_t rows[KR];
     raster_rows_span<WT, CT>(nl, p.R, rows, span);
 #pragma unroll
     for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k] | xrows[k]);
-    flatten<WT>(rows, flat);
     const int quad = quadrant(ax, ay, gx, gy);
     // uint2 word q of this lane is row word 2(q + 7h) .. +1: word j >= 1 expands cells
     // 4(j-1) .. 4(j-1)+3.  c holds this lane's cells from bit 0: lane 0 cells -4.. (its word 0
-    // is the quadrant one-hot), lane 1 cells 52..
-    const unsigned long long lo = (unsigned long long)flat[0] | ((unsigned long long)flat[1] << 32);
-    const unsigned long long hi = ((unsigned long long)flat[1] >> 20) | ((unsigned long long)flat[2] << 12) |
-                                  ((unsigned long long)flat[3] << 44);
-    const unsigned long long c = h ? hi : (lo << 4);
+    // is the quadrant one-hot), lane 1 cells 52..  Built straight from the row masks (window row r
+    // is distinct row max(r-1, 0), quirk Q1): V = sum_r Q_r << (10 r + 4) over this lane's six
+    // window rows Q (lane 0: rows 0-5; lane 1: rows 5-9 and 0), c = V >> 6h.
+    const uint32_t q0 = h ? rows[4] : rows[0], q1 = h ? rows[5] : rows[0], q2 = h ? rows[6] : rows[1];
+    const uint32_t q3 = h ? rows[7] : rows[2], q4 = h ? rows[8] : rows[3], q5 = h ? 0u : rows[4];
+    const uint32_t vlo = (q0 << 4) | (q1 << 14) | (q2 << 24);
+    const uint32_t vhi = (q2 >> 8) | (q3 << 2) | (q4 << 12) | (q5 << 22);
+    const unsigned long long c = (((unsigned long long)vhi << 32) | vlo) >> (6 * h);
+    // nibble jj of c is byte jj/2 of the even- / odd-nibble masks: one byte-select multiply and an AND
+    const uint32_t clo = (uint32_t)c, chi = (uint32_t)(c >> 32);
+    const uint32_t ne0 = clo & 0x0F0F0F0Fu, no0 = (clo >> 4) & 0x0F0F0F0Fu;
+    const uint32_t ne1 = chi & 0x0F0F0F0Fu, no1 = (chi >> 4) & 0x0F0F0F0Fu;
+    const uint32_t kx = 0x00204081u;
     auto word = [&](int jj) -> uint32_t {   // jj: this lane's word 0 .. 2*HQ-1
-      return (((uint32_t)(c >> (4 * jj)) & 0xFu) * 0x00204081u) & 0x01010101u;
+      const int b = jj >> 1;
+      const uint32_t src = (jj & 1) ? (b < 4 ? no0 : no1) : (b < 4 ? ne0 : ne1);
+      return mul24_byte(src, kx, b & 3) & 0x01010101u;
     };
     uint2* dst = reinterpret_cast<uint2*>(stage + (tid & 62) / 2 * F) + HQ * h;
 #pragma unroll
     for (int q = 0; q < HQ; ++q) {
-      const uint32_t w0 = q == 0 ? (h ? word(0) : 1u << (8 * quad)) : word(2 * q);
+      const uint32_t w0 = q == 0 ? (word(0) | (h ? 0u : 1u << (8 * quad))) : word(2 * q);   // (lane 0: word(0) = 0)
       if (q < NQ - HQ || !h) dst[q] = make_uint2(w0, word(2 * q + 1));
     }
   }
