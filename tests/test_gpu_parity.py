@@ -300,6 +300,33 @@ def test_distance_sqrt_exhaustive(gpu):
     env.close()
 
 
+@pytest.mark.parametrize("W", [10, 5])
+def test_goal_threshold_boundaries(gpu, W):
+    """done's goal test (dist < threshold_goal, ballenv_env.py:200-229) on the fixed-shape step kernels:
+    every offset |dx|, |dy| <= 60 against numpy's sqrt(d2) < threshold, at thresholds on and one ulp
+    either side of exact square roots (an integer d2 < n form of the test must match this too)."""
+    from gym_ballenv_amd.config import EnvConfig
+    r = np.arange(-60, 61)
+    dx, dy = [a.ravel() for a in np.meshgrid(r, r, indexing="ij")]
+    N = dx.size
+    d = np.sqrt((dx.astype(np.float64) ** 2 + dy.astype(np.float64) ** 2))
+    s1800 = float(np.sqrt(1800.0))
+    for thr in (10.0, np.nextafter(10.0, 0.0), np.nextafter(10.0, 20.0), s1800, np.nextafter(s1800, 0.0),
+                np.nextafter(s1800, 99.0), 7.5, 0.0, -1.0, 1e9):
+        cfg_py = EnvConfig(autoreset=False, time_limit=0, threshold_goal=float(thr))
+        env = make_env(cfg_py, N, W, gpu)
+        assert env.kernel_name("step") in ("step2_kernel<10, 13, 5>", "stepw_kernel<5, 13, 5, 8>", f"be_kernel<{W}, 0, 13, 5>")
+        st = np_state(env)
+        st["goal"][:] = (250, 250)
+        st["agent"] = np.stack([250 + dx, 250 + dy], 1).astype(np.int16)
+        st["static_obs"][:] = (470, 30)      # far from every agent: no collision, nothing near
+        st["dyn_obs"][:] = (30, 470)
+        load_np_state(env, st)
+        _, _, done, _ = env.step(torch.full((N,), 5, dtype=torch.uint8, device=gpu))   # the (0, 0) move
+        np.testing.assert_array_equal(done.cpu().numpy(), d < thr, err_msg=f"threshold {thr!r}")
+        env.close()
+
+
 def test_large_batch_subset_vs_oracle(gpu):
     """2^20 envs (past the Infinity Cache): a contiguous slice matches the oracle run
     on just that slice (Philox streams are keyed by global env id)."""
