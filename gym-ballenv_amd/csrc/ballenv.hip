@@ -362,10 +362,10 @@ __device__ __forceinline__ void raster_rows_mt(const NearList<BLOCK>& nl, int R,
 // an entry's rows cost one LDS read, one 64-bit shift and one OR each instead of the span arithmetic.
 template <int WT, int BLOCK>
 __device__ __forceinline__ void raster_rows_span(const NearList<BLOCK>& nl, int R, uint32_t (&rows)[Geo<WT>::K],
-                                                 const uint64_t* span) {
+                                                 const uint64_t* span, const uint32_t* init = nullptr) {
   constexpr int K = Geo<WT>::K;
 #pragma unroll
-  for (int k = 0; k < K; ++k) rows[k] = 0u;
+  for (int k = 0; k < K; ++k) rows[k] = init ? init[k] : 0u;   // (init: masks already within W bits)
   for (int n = 0; n < nl.cnt; ++n) {
     int f, e;
     nl.get(n, f, e);                                   // agent-relative: window (f + W/2, e + W/2)
@@ -1905,19 +1905,16 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   // ---- observation (prep_state4): own near list -> rows, OR-ed over the pair, half a row each
   {
     uint32_t rows[KR];
-    raster_rows_span<WT, CT>(nl, p.R, rows, span);
-#pragma unroll
-    for (int k = 0; k < KR; ++k) rows[k] = pair_or(rows[k] | xrows[k]);
-    const int quad = quadrant(ax, ay, gx, gy);
-    // uint2 word q of this lane is row word 2(q + 7h) .. +1: word j >= 1 expands cells
-    // 4(j-1) .. 4(j-1)+3.  c holds this lane's cells from bit 0: lane 0 cells -4.. (its word 0
-    // is the quadrant one-hot), lane 1 cells 52..  Built straight from the row masks (window row r
-    // is distinct row max(r-1, 0), quirk Q1): V = sum_r Q_r << (10 r + 4) over this lane's six
-    // window rows Q (lane 0: rows 0-5; lane 1: rows 5-9 and 0), c = V >> 6h.
-    const uint32_t q0 = h ? rows[4] : rows[0], q1 = h ? rows[5] : rows[0], q2 = h ? rows[6] : rows[1];
-    const uint32_t q3 = h ? rows[7] : rows[2], q4 = h ? rows[8] : rows[3], q5 = h ? 0u : rows[4];
-    const uint32_t vlo = (q0 << 4) | (q1 << 14) | (q2 << 24);
-    const uint32_t vhi = (q2 >> 8) | (q3 << 2) | (q4 << 12) | (q5 << 22);
+    raster_rows_span<WT, CT>(nl, p.R, rows, span, xrows);   // from a reset env's new rows (else 0)
+    // three 10-bit rows per word, OR-ed over the pair (3 DPP ops); then this lane's cells from its
+    // first nibble: lane 0 cells -4.. (its word 0 is the quadrant one-hot), lane 1 cells 52..  Window
+    // row r is distinct row max(r-1, 0) (quirk Q1): V = sum_r R_r << (10 r + 4) over the lane's six
+    // window rows (lane 0: 0-5; lane 1: 5-9), c = V >> 6h, from the packed words directly.
+    const uint32_t P0 = pair_or(rows[0] | (rows[1] << 10) | (rows[2] << 20));
+    const uint32_t P1 = pair_or(rows[3] | (rows[4] << 10) | (rows[5] << 20));
+    const uint32_t P2 = pair_or(rows[6] | (rows[7] << 10) | (rows[8] << 20));
+    const uint32_t vlo = h ? ((P1 >> 6) & 0xFFFFF0u) | (P2 << 24) : ((P0 << 4) & 0x3FF0u) | (P0 << 14);
+    const uint32_t vhi = h ? P2 >> 8 : (P0 >> 18) | (P1 << 12);
     const unsigned long long c = (((unsigned long long)vhi << 32) | vlo) >> (6 * h);
     // nibble jj of c is byte jj/2 of the even- / odd-nibble masks: one byte-select multiply and an AND
     const uint32_t clo = (uint32_t)c, chi = (uint32_t)(c >> 32);
@@ -1929,10 +1926,13 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
       const uint32_t src = (jj & 1) ? (b < 4 ? no0 : no1) : (b < 4 ? ne0 : ne1);
       return mul24_byte(src, kx, b & 3) & 0x01010101u;
     };
+    // quadrant(ax, ay, gx, gy) one-hot: byte 2 sy + (1 ^ sx ^ sy), s = the sign of goal - agent
+    const uint32_t sx = (uint32_t)(gx - ax) >> 31, sy = (uint32_t)(gy - ay) >> 31;
+    const uint32_t onehot = 1u << ((sy << 4) | ((sx ^ sy ^ 1u) << 3));
     uint2* dst = reinterpret_cast<uint2*>(stage + (tid & 62) / 2 * F) + HQ * h;
 #pragma unroll
     for (int q = 0; q < HQ; ++q) {
-      const uint32_t w0 = q == 0 ? (word(0) | (h ? 0u : 1u << (8 * quad))) : word(2 * q);   // (lane 0: word(0) = 0)
+      const uint32_t w0 = q == 0 ? (h ? word(0) : onehot) : word(2 * q);
       if (q < NQ - HQ || !h) dst[q] = make_uint2(w0, word(2 * q + 1));
     }
   }
