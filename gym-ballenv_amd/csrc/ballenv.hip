@@ -1795,18 +1795,24 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   DIAG(8);
   // ---- collision + window-box tests (be_kernel's packed int16x2 form), near list
   bool hs = false, hd = false;
+  // the near list's next free slot as an LDS address, advanced by sat(1 - over) slots: no compare /
+  // select / carry chain (and its VCC hazard nops) per obstacle
+  uint32_t* nlp = nl.base;
   auto obstacle_pk = [&](int32_t opk, bool real, bool& hit) {
     const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
     hit |= real & ((uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2);
     const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
     const v2u over = __builtin_elementwise_sub_sat(b, boxw);   // (0, 0) iff inside the box
-    nl.base[nl.cnt * CT] = __builtin_bit_cast(uint32_t, d);
-    nl.cnt += (real & (__builtin_bit_cast(uint32_t, over) == 0u)) ? 1 : 0;
+    *nlp = __builtin_bit_cast(uint32_t, d);
+    // 1 iff inside the box (and a real slot): a saturating 1 - over, one VALU without VCC
+    const uint32_t in = __builtin_elementwise_sub_sat(1u, __builtin_bit_cast(uint32_t, over) | (real ? 0u : 1u));
+    nlp += CT * in;
   };
 #pragma unroll
   for (int j = 0; j < SD; ++j) obstacle_pk(dnew[j], L * j + h < NDC, hd);
 #pragma unroll
   for (int j = 0; j < SS; ++j) obstacle_pk(so[j], L * j + h < NSC, hs);
+  nl.cnt = (int)((nlp - nl.base) / CT);
   hs = pair_or((uint32_t)hs) != 0u;
   hd = pair_or((uint32_t)hd) != 0u;
   DIAG(10);
