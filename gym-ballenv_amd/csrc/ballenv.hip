@@ -1224,13 +1224,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const v2s boxo = {(short)bxo, (short)byo};
       const v2u boxw = {(unsigned short)bw, (unsigned short)bh};
       // near-list entries are agent-relative (dx, dy) here; the raster adds the window offset
+      // (the near list's next slot as an LDS address advanced by sat(1 - over) slots, as in
+      // step2_kernel: no compare / select / carry chain per obstacle; nl.cnt is set after the tests)
+      uint32_t* nlp = nl.base;
       auto obstacle_pk = [&](int32_t opk, bool& hit) {
         const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
         hit |= (uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2;
         const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
         const v2u over = __builtin_elementwise_sub_sat(b, boxw);   // (0, 0) iff inside the box
-        nl.base[nl.cnt * BLOCK_THREADS] = __builtin_bit_cast(uint32_t, d);
-        nl.cnt += __builtin_bit_cast(uint32_t, over) == 0u ? 1 : 0;
+        *nlp = __builtin_bit_cast(uint32_t, d);
+        nlp += BLOCK_THREADS * __builtin_elementwise_sub_sat(1u, __builtin_bit_cast(uint32_t, over));
       };
       if constexpr (FIXED) {
         DIAG(7);
@@ -1250,6 +1253,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         DIAG(11);
 #pragma unroll
         for (int j = 0; j < NSC; ++j) obstacle_pk(so[j], hs);
+        nl.cnt = (int)((nlp - nl.base) / BLOCK_THREADS);
       }
       // generic slot loops: slots past the obstacle count hold a far-away sentinel, so the
       // collision / window tests are branch-free; only their stores are skipped
