@@ -395,6 +395,13 @@ __device__ __forceinline__ void raster_rows_span(const NearList<BLOCK>& nl, int 
   for (int k = 0; k < K; ++k) rows[k] &= (1u << WT) - 1u;
 }
 
+// dx^2 + dy^2 of a packed int16 pair as the VOP3P dot with an inline-zero accumulator (the compiler
+// picks the VOP2 accumulate form, which costs a zeroing move per call)
+__device__ __forceinline__ int dot2_sq(v2s d) {
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(r) : "v"(d));
+  return r;
+}
 // Flatten rows into prep_state4's cell order (window row r uses distinct row max(r-1,0): quirk Q1).
 template <int WT>
 __device__ __forceinline__ void flatten(const uint32_t (&rows)[Geo<WT>::K], uint32_t (&flat)[Geo<WT>::NW]) {
@@ -1229,7 +1236,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       uint32_t* nlp = nl.base;
       auto obstacle_pk = [&](int32_t opk, bool& hit) {
         const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
-        hit |= (uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2;
+        hit |= (uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2;   // (dot2_sq: neutral here, r05_dot2_vop3p_ab.txt)
         const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
         const v2u over = __builtin_elementwise_sub_sat(b, boxw);   // (0, 0) iff inside the box
         *nlp = __builtin_bit_cast(uint32_t, d);
@@ -1821,7 +1828,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   uint32_t* nlp = nl.base;
   auto obstacle_pk = [&](int32_t opk, bool real, bool& hit) {
     const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
-    hit |= real & ((uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2);
+    hit |= real & ((uint32_t)dot2_sq(d) <= R2);
     const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
     const v2u over = __builtin_elementwise_sub_sat(b, boxw);   // (0, 0) iff inside the box
     *nlp = __builtin_bit_cast(uint32_t, d);
