@@ -1672,8 +1672,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
 //    a read, a shift and an OR per row; 6.18 against 6.39 us at 65 536 envs, 5.09 against 5.24 at
 //    32 768 -- profiles/r05_step2_span_raster_ab.txt), so pick_kernel takes this kernel only while
 //    W-1+2R <= 63 (R <= 27; the defaults' R is 25), the one-lane kernel past it;
-//  * lane h writes its half of the obs row (uint2 words [7h, 7h+7)) into the wave's stage and
-//    half of the per-env scalar stores (a per-lane pointer select: one store instruction);
+//  * lane h writes its half of the obs row (uint2 words [7h, 7h+7)) into the wave's stage; both
+//    lanes store every per-env scalar (the same value to the same address: one full-wave store per
+//    array, 5.98 -> 5.90 us against splitting the arrays over the pair by per-lane pointer selects,
+//    profiles/r05_step2_dup_stores_ab.txt);
 //  * the Philox block, the agent move, the f64 reward and done run on both lanes (the same
 //    instruction stream, so no extra issue).
 // Autoreset is wave_resets with the even lanes as owners; stats fold per wave (32 envs =
@@ -1855,17 +1857,18 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   const bool trunc = p.time_limit > 0 && len >= p.time_limit;
   const bool done = env_done || trunc;
   const bool do_reset = valid && done && p.autoreset;
-  if (valid) {   // the pair splits the stores: lane 0 reward/agent/done/prev_dist, lane 1 the rest
-    double* pd = h ? p.ep_return : p.reward;
-    st_wt(pd + i, h ? ret : reward);
-    int32_t* pi = h ? p.ep_len : p.agent;
-    st_wt(pi + i, h ? len : pk(ax, ay));
-    uint8_t* pb = h ? p.truncated : p.done;
-    if (pb) st_wt(pb + i, (uint8_t)(h ? (trunc && !env_done) : done));
-    if (!h) st_wt(p.prev_dist + i, dist);
+  if (valid) {   // both lanes of the pair store the env's scalars (the same value to the same address:
+                 // one full-wave store per array, no per-lane pointer selects or exec masking)
+    st_wt(p.reward + i, reward);
+    st_wt(p.ep_return + i, ret);
+    st_wt(p.agent + i, pk(ax, ay));
+    st_wt(p.ep_len + i, len);
+    if (p.done) st_wt(p.done + i, (uint8_t)done);
+    if (p.truncated) st_wt(p.truncated + i, (uint8_t)(trunc && !env_done));
+    st_wt(p.prev_dist + i, dist);
     if (done) {
-      if (!h && p.final_return) st_wt(p.final_return + i, ret);
-      if (h && p.final_len) st_wt(p.final_len + i, len);
+      if (p.final_return) st_wt(p.final_return + i, ret);
+      if (p.final_len) st_wt(p.final_len + i, len);
     }
     // (stored after done is known: measured faster than storing inside the obstacle loop)
 #pragma unroll
