@@ -1912,16 +1912,12 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
-      // both lanes take the new agent / goal / rows; the scalars are split over the pair as in the
-      // physics above (lane 1: ep_return / ep_len).  Ordering against the physics stores is the
-      // wave's program order (wave_resets' note), whichever lane stores
+      // both lanes take the new agent / goal / rows and store the env's scalars, as in the physics
+      // above.  Ordering against the physics stores is the wave's program order (wave_resets' note)
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
-      if (h) {
-        st_wt(p.ep_return + i, 0.0);
-        st_wt(p.ep_len + i, 0);
-        return;
-      }
+      st_wt(p.ep_return + i, 0.0);
+      st_wt(p.ep_len + i, 0);
       st_wt(p.agent + i, ag);
       st_wt(p.prev_dist + i, prev);
       st_wt(p.goal + i, go);
@@ -2180,14 +2176,17 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const bool trunc = p.time_limit > 0 && len >= p.time_limit;
   const bool done = env_done || trunc;
   const bool do_reset = valid && done && p.autoreset;
-  if (valid) {   // the per-env scalars over the group's lanes: one store instruction per class
-    if (h < 3) st_wt((h == 0 ? p.reward : h == 1 ? p.ep_return : p.prev_dist) + i, h == 0 ? reward : h == 1 ? ret : dist);
-    if (h < 2) st_wt((h ? p.ep_len : p.agent) + i, h ? len : pk(ax, ay));
-    uint8_t* pb = h == 0 ? p.done : h == 1 ? p.truncated : nullptr;
-    if (pb) st_wt(pb + i, (uint8_t)(h ? (trunc && !env_done) : done));
+  if (valid) {   // the per-env scalars: one full-wave store per array
+    st_wt(p.reward + i, reward);   // every lane of the group: the same value to the same address
+    st_wt(p.ep_return + i, ret);
+    st_wt(p.prev_dist + i, dist);
+    st_wt(p.agent + i, pk(ax, ay));
+    st_wt(p.ep_len + i, len);
+    if (p.done) st_wt(p.done + i, (uint8_t)done);
+    if (p.truncated) st_wt(p.truncated + i, (uint8_t)(trunc && !env_done));
     if (done) {
-      if (h == 2 && p.final_return) st_wt(p.final_return + i, ret);
-      if (h == 3 && p.final_len) st_wt(p.final_len + i, len);
+      if (p.final_return) st_wt(p.final_return + i, ret);
+      if (p.final_len) st_wt(p.final_len + i, len);
     }
 #pragma unroll
     for (int j = 0; j < SD; ++j) {
@@ -2234,22 +2233,18 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
-      // every lane of the group takes the new agent / goal / rows; the scalars are spread over the
-      // group as in the physics above (lane 0 agent, lane 1 ep_return / ep_len, lane 2 prev_dist).
-      // Ordering against the physics stores is the wave's program order (wave_resets' note)
+      // every lane of the group takes the new agent / goal / rows and stores the env's scalars, as
+      // in the physics above.  Ordering against the physics stores is the wave's program order
+      // (wave_resets' note)
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
-      if (h == 0) {
-        st_wt(p.agent + i, ag);
-        st_wt(p.goal + i, go);
-        st_wt(p.total_dist + i, td);
-        st_wt(p.episode + i, episode + 1u);
-      } else if (h == 1) {
-        st_wt(p.ep_return + i, 0.0);
-        st_wt(p.ep_len + i, 0);
-      } else if (h == 2) {
-        st_wt(p.prev_dist + i, prev);
-      }
+      st_wt(p.agent + i, ag);
+      st_wt(p.goal + i, go);
+      st_wt(p.total_dist + i, td);
+      st_wt(p.episode + i, episode + 1u);
+      st_wt(p.ep_return + i, 0.0);
+      st_wt(p.ep_len + i, 0);
+      st_wt(p.prev_dist + i, prev);
     };
     if (!(m & (m - 1)))
       wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
