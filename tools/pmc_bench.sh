@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pmc; export TMPDIR=/tmp
-ARGS="--no-cpu-baseline --mode eager --steps 200 --warmup 20 --policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 0 --config4-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0 ${BENCH_ARGS:-}"
+ARGS="--no-cpu-baseline --mode eager --steps 200 --warmup 20 --policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 0 --config4-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0 --shard-steps 0 --eager-steps 0 ${BENCH_ARGS:-}"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc/$c -o run -- python3 bench.py $ARGS \
       > gpurun_out/pmc/$c.log 2>&1

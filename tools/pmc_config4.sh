@@ -7,7 +7,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=${ROUND:-r04}
-COMMON="--no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 --torch-policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0 --config4-steps 200"
+COMMON="--no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 --torch-policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0 --shard-steps 0 --eager-steps 0 --config4-steps 200"
 for n in ${SIZES:-262144 131072 65536 32768}; do
   PASSES="FETCH_SIZE WRITE_SIZE" timeout -k 10 400 bash tools/pmc_passes.sh pmc_c4/g$n $COMMON --config4-envs $n || exit 1
   k="be_kernel<10, 0, 13, 5>"; [ $n -le 98304 ] && k="step2_kernel<10, 13, 5>"
