@@ -10,6 +10,8 @@ R=${ROUND:-r04}
 COMMON="--no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 --torch-policy-steps 0 --board-steps 0 --rollout-steps 0 --cold-steps 0 --config2-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0 --shard-steps 0 --eager-steps 0 --config4-steps 200"
 for n in ${SIZES:-262144 131072 65536 32768}; do
   PASSES="FETCH_SIZE WRITE_SIZE" timeout -k 10 400 bash tools/pmc_passes.sh pmc_c4/g$n $COMMON --config4-envs $n || exit 1
-  k="be_kernel<10, 0, 13, 5>"; [ $n -le 98304 ] && k="step2_kernel<10, 13, 5>"
-  python3 tools/pmc_report.py gpurun_out/pmc_c4/g$n "$k" $n --out gpurun_out/pmc_c4/${R}_pmc_config4_$n.json | tail -2
+  # grid = the kernel's threads at this size (step2: 2 lanes per env, 128-env blocks; one lane: 256-env blocks)
+  k="be_kernel<10, 0, 13, 5>"; g=$(( (n + 255) / 256 * 256 ))
+  [ $n -le 98304 ] && { k="step2_kernel<10, 13, 5>"; g=$(( (n + 127) / 128 * 256 )); }
+  python3 tools/pmc_report.py gpurun_out/pmc_c4/g$n "$k" $n --grid $g --out gpurun_out/pmc_c4/${R}_pmc_config4_$n.json | tail -2
 done

@@ -1,8 +1,10 @@
 """Per-kernel summary of tools/pmc_passes.sh passes.
 
-    python tools/pmc_report.py <pass root> <kernel regex> <units per dispatch> [--first N] [--out f.json]
+    python tools/pmc_report.py <pass root> <kernel regex> <units per dispatch> [--first N] [--grid G] [--out f.json]
 
-Averages each counter over the first N matching dispatches (default: all), per dispatch.
+Averages each counter over the first N matching dispatches (default: all), per dispatch; --grid keeps
+only dispatches of that Grid_Size (threads), so another leg's launches of the same kernel at another
+batch size (the bench's short headline leg beside a config-4 shard leg) stay out of the average.
 HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (kB; gfx950 FETCH_SIZE reports half of wide reads,
 MI355X_MICROARCH.md 'HBM').  SQ_*_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles,
 SQ_VALU_MFMA_BUSY_CYCLES cycles (MI355X_MICROARCH.md 'per-instruction cycle constants');
@@ -21,6 +23,7 @@ ap.add_argument("root")
 ap.add_argument("pattern")
 ap.add_argument("units", type=float)
 ap.add_argument("--first", type=int, default=0)
+ap.add_argument("--grid", type=int, default=0)
 ap.add_argument("--out")
 a = ap.parse_args()
 
@@ -31,7 +34,7 @@ for d in sorted(glob.glob(os.path.join(a.root, "*", ""))):
         continue
     per = {}
     for r in csv.DictReader(open(files[0])):
-        if re.search(a.pattern, r["Kernel_Name"]):
+        if re.search(a.pattern, r["Kernel_Name"]) and (not a.grid or int(r["Grid_Size"]) == a.grid):
             name = r["Kernel_Name"]
             key = (r["Counter_Name"], int(r["Dispatch_Id"]))
             per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
@@ -43,7 +46,8 @@ for d in sorted(glob.glob(os.path.join(a.root, "*", ""))):
         vals[c] = statistics.mean(per[(c, i)] for i in ids)
         ndisp[c] = len(ids)
 
-out = {"kernel": name, "units_per_dispatch": a.units, "dispatches": ndisp, "counters_per_dispatch": vals}
+out = {"kernel": name, "units_per_dispatch": a.units, "grid_size": a.grid or None, "dispatches": ndisp,
+       "counters_per_dispatch": vals}
 g = vals.get
 if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
     hbm = (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
