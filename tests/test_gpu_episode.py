@@ -235,7 +235,7 @@ def test_step_kernel_time_limit_boundary(gpu):
     env.close()
 
 
-@pytest.mark.parametrize("G", [0, 1, 3, 7])
+@pytest.mark.parametrize("G", [0, 1, 3, 5, 7, 11, 50])
 @pytest.mark.parametrize("W", [10, 5])
 def test_goal_change_steps_vs_oracle(gpu, G, W):
     """Short goal-change periods with caller actions (so the fixed-shape kernel runs): every
