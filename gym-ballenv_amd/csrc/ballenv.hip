@@ -233,6 +233,12 @@ __device__ __forceinline__ double calc_dist(int x1, int y1, int x2, int y2) {
   double dx = (double)(x1 - x2), dy = (double)(y1 - y2);
   return sqrt_int(dx * dx + dy * dy);
 }
+// The same with the library sqrt (the same bits): the fused rollouts keep it -- sqrt_int measured
+// within noise to slightly slower there (profiles/r05_rollout_sqrt_ab.txt)
+__device__ __forceinline__ double calc_dist_lib(int x1, int y1, int x2, int y2) {
+  double dx = (double)(x1 - x2), dy = (double)(y1 - y2);
+  return sqrt(dx * dx + dy * dy);
+}
 
 // Window geometry shared by the near test and the rasteriser.
 struct Win {
@@ -845,9 +851,10 @@ __device__ void stage_full_row(uint8_t* dst, const uint32_t (&flat)[Geo<WT>::NW]
 
 // A reset env's distances: returns total_distance = |agent - goal| and sets prev to the
 // pre-resample distance (Q9; equal to total unless the agent was re-drawn).
+template <bool LIB = false>
 __device__ __forceinline__ double reset_dists(int32_t ag, int32_t go, int32_t a0, double& prev) {
-  const double td = calc_dist(px(ag), py(ag), px(go), py(go));
-  prev = a0 == ag ? td : calc_dist(px(go), py(go), px(a0), py(a0));
+  const double td = LIB ? calc_dist_lib(px(ag), py(ag), px(go), py(go)) : calc_dist(px(ag), py(ag), px(go), py(go));
+  prev = a0 == ag ? td : (LIB ? calc_dist_lib(px(go), py(go), px(a0), py(a0)) : calc_dist(px(go), py(go), px(a0), py(a0)));
   return td;
 }
 
@@ -2428,7 +2435,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
     ax = min(max(ax + (int)((p.amx >> sh) & 3u) - 1, 0), p.screen_w);
     ay = min(max(ay + (int)((p.amy >> sh) & 3u) - 1, 0), p.screen_h);
     const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
-    const double dist = calc_dist(gx, gy, ax, ay);
+    const double dist = calc_dist_lib(gx, gy, ax, ay);
     const double rbase = (0.0 - p.time_penalty) + (old_dist - dist) / total;
     PH(1);
     // ---- collision test and row masks (stepw_kernel's)
@@ -2503,7 +2510,7 @@ __global__ __launch_bounds__(32 * L) void rolloutw_kernel(KParams p) {
       bool reset_now = false;
       auto esink = [&](int own, int32_t ag, int32_t go, int32_t a0) {   // every lane of the env's group
         goal = go;
-        total = reset_dists(ag, go, a0, old_dist);
+        total = reset_dists<true>(ag, go, a0, old_dist);
         ret = 0.0; len = 0; ++episode; was_reset = true; reset_now = true; counter = 0;
 #pragma unroll
         for (int j = 0; j < SS; ++j) so[j] = ost[own * G + min(L * j + h, NSC - 1)];
@@ -2897,7 +2904,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
 
     // ---- distance, reward, done (ballenv_env.py:268-286, 200-229)
     // (computing this right after the move, as step2_kernel does, measured slower here)
-    const double dist = calc_dist(gx, gy, ax, ay);
+    const double dist = calc_dist_lib(gx, gy, ax, ay);
     double reward = 0.0 - p.time_penalty;
     reward += (old_dist - dist) / total;
     if (hs) reward -= p.static_penalty;          // statics come first in obstacle_list (Q3)
@@ -2946,7 +2953,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
       auto osink = [&](int sl, int k, int, int32_t o) { ost[sl * G + k] = o; };
       auto esink = [&](int own, int32_t ag, int32_t go, int32_t a0) {
         goal = go;
-        total = reset_dists(ag, go, a0, old_dist);
+        total = reset_dists<true>(ag, go, a0, old_dist);
         ret = 0.0; len = 0; ++episode; was_reset = true;
 #pragma unroll
         for (int k = 0; k < NSC; ++k) so[k] = ost[own * G + k];
