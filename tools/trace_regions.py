@@ -7,7 +7,9 @@ bench.py's headline leg launches the step kernel `warmup` times eagerly, replays
 for `untimed` steps (settle), then times `steps` launches: launches warmup+untimed+1 ..
 warmup+untimed+steps of the headline kernel are the timed region.  The config-2 and large-batch legs
 are the last 1000 / 200 launches of their kernels; config 4 at one rank (262 144 envs, the one-lane
-kernel) is the 1000 launches of that kernel before the large-batch leg's 2 x 200."""
+kernel) and its per-rank shards (131 072 envs one-lane, 32 768 envs step2_kernel) are the last 1000
+launches of that kernel at that grid size (threads: Grid_Size; the one-lane kernel runs 1 thread per env,
+step2_kernel 2)."""
 import argparse
 import csv
 import statistics
@@ -21,10 +23,14 @@ ap.add_argument("--steps", type=int, default=1000)
 a = ap.parse_args()
 
 runs = defaultdict(list)
+by_grid = defaultdict(list)
 for r in csv.DictReader(open(a.trace)):
-    runs[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-for k in runs:
-    runs[k].sort()
+    t = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+    runs[r["Kernel_Name"]].append(t)
+    if "Grid_Size" in r:
+        by_grid[(r["Kernel_Name"], int(r["Grid_Size"]))].append(t)
+for k in list(runs) + list(by_grid):
+    (runs if k in runs else by_grid)[k].sort()
 
 
 def avg_us(launches):
@@ -43,11 +49,15 @@ if head:
     print(f"{head}: {len(L)} launches in the whole command; the headline's timed region (launches "
           f"{lo + 1}..{lo + len(reg)}) averages {avg_us(reg):.3f} us per launch; "
           f"65536 x 390 B / that = {65536 * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
-c4 = find("be_kernel<10, 0, 13, 5>")
-if c4 and len(runs[c4]) >= 1400:
-    reg = runs[c4][-1400:-400]
-    print(f"{c4} (config 4 at one rank, 262144 envs): the 1000 launches before the large-batch leg average "
-          f"{avg_us(reg):.3f} us; 262144 x 390 B / that = {262144 * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
+for prefix, n, grid, what in (("be_kernel<10, 0, 13, 5>", 262144, 262144, "config 4 at one rank"),
+                              ("be_kernel<10, 0, 13, 5>", 131072, 131072, "config 4's 2-GPU shard"),
+                              ("step2_kernel<10, 13, 5>", 32768, 65536, "config 4's 8-GPU shard")):
+    k = find(prefix)
+    L = by_grid.get((k, grid), [])
+    if len(L) >= 1000:
+        reg = L[-1000:]
+        print(f"{k} ({what}, {n} envs): the last 1000 launches at that size average {avg_us(reg):.3f} us; "
+              f"{n} x 390 B / that = {n * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
 for prefix, last, what in (("stepw_kernel<5, 13, 5, 8>", 1000, "config 2, 4096 envs, W=5"),
                            ("be_kernel<10, 0, 13, 5>", 200, "2^20 envs, large_batch"),
                            ("board_kernel<6, false, 1>", 1000, "createBoard step, 65536 envs"),
