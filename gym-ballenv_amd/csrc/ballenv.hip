@@ -272,6 +272,12 @@ __device__ __forceinline__ int quadrant(int ax, int ay, int gx, int gy) {
   return 2;
 }
 
+// Byte distance between two pointers into LDS, in 32 bits (a pointer difference goes through the
+// 64-bit flat aperture: ~15 instructions with the signed-division fixup).
+__device__ __forceinline__ uint32_t lds_bytes(const void* lo, const void* hi) {
+  return (uint32_t)(uintptr_t)hi - (uint32_t)(uintptr_t)lo;
+}
+
 // Per-thread list of window-relevant obstacles in LDS, laid out [slot][BLOCK].
 template <int BLOCK>
 struct NearList {
@@ -1267,7 +1273,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
         DIAG(11);
 #pragma unroll
         for (int j = 0; j < NSC; ++j) obstacle_pk(so[j], hs);
-        nl.cnt = (int)((nlp - nl.base) / BLOCK_THREADS);
+        nl.cnt = (int)(lds_bytes(nl.base, nlp) / (BLOCK_THREADS * 4u));
       }
       // generic slot loops: slots past the obstacle count hold a far-away sentinel, so the
       // collision / window tests are branch-free; only their stores are skipped
@@ -1849,7 +1855,7 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   for (int j = 0; j < SD; ++j) obstacle_pk(dnew[j], L * j + h < NDC, hd);
 #pragma unroll
   for (int j = 0; j < SS; ++j) obstacle_pk(so[j], L * j + h < NSC, hs);
-  nl.cnt = (int)((nlp - nl.base) / CT);
+  nl.cnt = (int)(lds_bytes(nl.base, nlp) / (CT * 4u));
   hs = pair_or((uint32_t)hs) != 0u;
   hd = pair_or((uint32_t)hd) != 0u;
   DIAG(10);
