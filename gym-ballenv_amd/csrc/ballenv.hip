@@ -169,6 +169,12 @@ template <class T>
 __device__ __forceinline__ T& ld_s_ptr(T* base, uint32_t idx) {   // (stores: the same addressing)
   return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (size_t)(idx * (uint32_t)sizeof(T)));
 }
+// write-through store at element idx of a uniform base, as base + zext(32-bit byte offset): the
+// SGPR-base store form, one 32-bit offset per element size instead of a 64-bit address per store
+template <class T>
+__device__ __forceinline__ void st_ws(T* base, uint32_t idx, T v) {
+  st_wt(&ld_s_ptr(base, idx), v);
+}
 __device__ __forceinline__ int isqrt_small(int n) {  // floor(sqrt(n)), 0 <= n < 2^22
   int s = (int)__builtin_amdgcn_sqrtf((float)n);
   if (s * s > n) --s;
@@ -1872,16 +1878,17 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   const bool do_reset = valid && done && p.autoreset;
   if (valid) {   // both lanes of the pair store the env's scalars (the same value to the same address:
                  // one full-wave store per array, no per-lane pointer selects or exec masking)
-    st_wt(p.reward + i, reward);
-    st_wt(p.ep_return + i, ret);
-    st_wt(p.agent + i, pk(ax, ay));
-    st_wt(p.ep_len + i, len);
-    if (p.done) st_wt(p.done + i, (uint8_t)done);
-    if (p.truncated) st_wt(p.truncated + i, (uint8_t)(trunc && !env_done));
-    st_wt(p.prev_dist + i, dist);
+    const uint32_t iu = (uint32_t)i;
+    st_ws(p.reward, iu, reward);
+    st_ws(p.ep_return, iu, ret);
+    st_ws(p.agent, iu, pk(ax, ay));
+    st_ws(p.ep_len, iu, len);
+    if (p.done) st_ws(p.done, iu, (uint8_t)done);
+    if (p.truncated) st_ws(p.truncated, iu, (uint8_t)(trunc && !env_done));
+    st_ws(p.prev_dist, iu, dist);
     if (done) {
-      if (p.final_return) st_wt(p.final_return + i, ret);
-      if (p.final_len) st_wt(p.final_len + i, len);
+      if (p.final_return) st_ws(p.final_return, iu, ret);
+      if (p.final_len) st_ws(p.final_len, iu, len);
     }
     // (stored after done is known: measured faster than storing inside the obstacle loop)
 #pragma unroll
@@ -1916,12 +1923,12 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     if (!h) write_row_global<WT>(p.terminal_obs + (int64_t)i * F, flat, quadrant(ax, ay, gx, gy));
   }
   if (m) {   // wave-cooperative: this wave runs its own resets
-    auto osink = [&](int, int k, int il, int32_t o) {
+    auto osink = [&](int, int k, int il, int32_t o) {   // (32-bit element offsets: pick_kernel keeps NS*N < 2^30)
       if (k < NSC) {
-        st_wt(p.static_obs + (size_t)k * N + il, o);
+        st_ws(p.static_obs, (uint32_t)k * (uint32_t)N + (uint32_t)il, o);
       } else {
-        st_wt(p.dyn_obs + (size_t)(k - NSC) * N + il, o);
-        st_wt(p.dyn_goal + (size_t)(k - NSC) * N + il, (uint8_t)(k - NSC));
+        st_ws(p.dyn_obs, (uint32_t)(k - NSC) * (uint32_t)N + (uint32_t)il, o);
+        st_ws(p.dyn_goal, (uint32_t)(k - NSC) * (uint32_t)N + (uint32_t)il, (uint8_t)(k - NSC));
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
@@ -1929,13 +1936,14 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
       // above.  Ordering against the physics stores is the wave's program order (wave_resets' note)
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
-      st_wt(p.ep_return + i, 0.0);
-      st_wt(p.ep_len + i, 0);
-      st_wt(p.agent + i, ag);
-      st_wt(p.prev_dist + i, prev);
-      st_wt(p.goal + i, go);
-      st_wt(p.total_dist + i, td);
-      st_wt(p.episode + i, episode + 1u);
+      const uint32_t iu = (uint32_t)i;
+      st_ws(p.ep_return, iu, 0.0);
+      st_ws(p.ep_len, iu, 0);
+      st_ws(p.agent, iu, ag);
+      st_ws(p.prev_dist, iu, prev);
+      st_ws(p.goal, iu, go);
+      st_ws(p.total_dist, iu, td);
+      st_ws(p.episode, iu, episode + 1u);
     };
     if (!(m & (m - 1)))
       wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
