@@ -1269,12 +1269,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
           int ox = px(dp[j]), oy = py(dp[j]);
           ngs[j] = dyn_move_fixed(p, t, ox, oy, dgi[j], t.speed[j], change, wj[j], st_flags);
           const int32_t npk = pk(ox, oy);
-          if (valid) st_wt(p.dyn_obs + (size_t)j * N + i, npk);
+          if (valid) st_ws(p.dyn_obs + (size_t)j * N, (uint32_t)i, npk);
           obstacle_pk(npk, hd);
         }
         if (valid && change) {   // every obstacle re-picks its goal on the same step
 #pragma unroll
-          for (int j = 0; j < NDC; ++j) st_wt(p.dyn_goal + (size_t)j * N + i, (uint8_t)ngs[j]);
+          for (int j = 0; j < NDC; ++j) st_ws(p.dyn_goal + (size_t)j * N, (uint32_t)i, (uint8_t)ngs[j]);
         }
         DIAG(11);
 #pragma unroll
@@ -1347,13 +1347,18 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       const bool trunc = p.time_limit > 0 && len >= p.time_limit;
       done = env_done || trunc;
       if (lead) {
-        st_wt(p.reward + i, reward);
-        st_wt(p.done + i, (uint8_t)done);
-        if (p.truncated) st_wt(p.truncated + i, (uint8_t)(trunc && !env_done));
-        st_wt(p.agent + i, pk(ax, ay));
-        st_wt(p.prev_dist + i, dist);
-        st_wt(p.ep_return + i, ret);
-        st_wt(p.ep_len + i, len);
+        // FIXED: SGPR-base stores with 32-bit offsets (FIX_MAX_ENVS); the generic kernels index in 64 bits
+        auto sto = [&](auto* base, auto v) {
+          if constexpr (FIXED) st_ws(base, (uint32_t)i, v);
+          else st_wt(base + i, v);
+        };
+        sto(p.reward, reward);
+        sto(p.done, (uint8_t)done);
+        if (p.truncated) sto(p.truncated, (uint8_t)(trunc && !env_done));
+        sto(p.agent, pk(ax, ay));
+        sto(p.prev_dist, dist);
+        sto(p.ep_return, ret);
+        sto(p.ep_len, len);
         if (done) {
           if (p.final_return) st_wt(p.final_return + i, ret);
           if (p.final_len) st_wt(p.final_len + i, len);
@@ -2198,16 +2203,17 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const bool done = env_done || trunc;
   const bool do_reset = valid && done && p.autoreset;
   if (valid) {   // the per-env scalars: one full-wave store per array
-    st_wt(p.reward + i, reward);   // every lane of the group: the same value to the same address
-    st_wt(p.ep_return + i, ret);
-    st_wt(p.prev_dist + i, dist);
-    st_wt(p.agent + i, pk(ax, ay));
-    st_wt(p.ep_len + i, len);
-    if (p.done) st_wt(p.done + i, (uint8_t)done);
-    if (p.truncated) st_wt(p.truncated + i, (uint8_t)(trunc && !env_done));
+    const uint32_t iu = (uint32_t)i;   // every lane of the group: the same value to the same address
+    st_ws(p.reward, iu, reward);
+    st_ws(p.ep_return, iu, ret);
+    st_ws(p.prev_dist, iu, dist);
+    st_ws(p.agent, iu, pk(ax, ay));
+    st_ws(p.ep_len, iu, len);
+    if (p.done) st_ws(p.done, iu, (uint8_t)done);
+    if (p.truncated) st_ws(p.truncated, iu, (uint8_t)(trunc && !env_done));
     if (done) {
-      if (p.final_return) st_wt(p.final_return + i, ret);
-      if (p.final_len) st_wt(p.final_len + i, len);
+      if (p.final_return) st_ws(p.final_return, iu, ret);
+      if (p.final_len) st_ws(p.final_len, iu, len);
     }
 #pragma unroll
     for (int j = 0; j < SD; ++j) {
@@ -2245,12 +2251,12 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
 #pragma unroll
     for (int k = 0; k < KR; ++k) xrows[k] = 0u;
     int kept = 1;   // wave_resets zeroes it for the lanes of a reset env
-    auto osink = [&](int, int k, int il, int32_t o) {
+    auto osink = [&](int, int k, int il, int32_t o) {   // (32-bit element offsets: NS*N < 2^30 here)
       if (k < NSC) {
-        st_wt(p.static_obs + (size_t)k * N + il, o);
+        st_ws(p.static_obs, (uint32_t)k * (uint32_t)N + (uint32_t)il, o);
       } else {
-        st_wt(p.dyn_obs + (size_t)(k - NSC) * N + il, o);
-        st_wt(p.dyn_goal + (size_t)(k - NSC) * N + il, (uint8_t)(k - NSC));
+        st_ws(p.dyn_obs, (uint32_t)(k - NSC) * (uint32_t)N + (uint32_t)il, o);
+        st_ws(p.dyn_goal, (uint32_t)(k - NSC) * (uint32_t)N + (uint32_t)il, (uint8_t)(k - NSC));
       }
     };
     auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {
@@ -2259,13 +2265,14 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
       // (wave_resets' note)
       double prev;
       const double td = reset_dists(ag, go, a0, prev);
-      st_wt(p.agent + i, ag);
-      st_wt(p.goal + i, go);
-      st_wt(p.total_dist + i, td);
-      st_wt(p.episode + i, episode + 1u);
-      st_wt(p.ep_return + i, 0.0);
-      st_wt(p.ep_len + i, 0);
-      st_wt(p.prev_dist + i, prev);
+      const uint32_t iu = (uint32_t)i;
+      st_ws(p.agent, iu, ag);
+      st_ws(p.goal, iu, go);
+      st_ws(p.total_dist, iu, td);
+      st_ws(p.episode, iu, episode + 1u);
+      st_ws(p.ep_return, iu, 0.0);
+      st_ws(p.ep_len, iu, 0);
+      st_ws(p.prev_dist, iu, prev);
     };
     if (!(m & (m - 1)))
       wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
@@ -3088,6 +3095,10 @@ struct Launch { KFn fn; int epb; int lds; char name[48]; int threads = BLOCK_THR
 
 // Fixed-shape step kernels for the reference's default obstacle counts (ball_cnn_ac3.py:40-41).
 constexpr int FIX_NS = 13, FIX_ND = 5;   // the reference's obstacle counts (ball_cnn_ac3.py:40-41)
+// The fixed-shape kernels address per-env arrays as a uniform base + a 32-bit byte offset (ld_s /
+// st_ws): element i of an 8-byte array needs i < 2^29.  Larger batches (~150 GB of state and outputs)
+// take the generic kernels, which index in 64 bits.
+constexpr int64_t FIX_MAX_ENVS = 1ll << 29;
 
 Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lanes10 = 1, int lpe5 = 0) {
   int W = c.window;
@@ -3095,7 +3106,8 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lane
   Launch L{nullptr, 0, 0, {0}};
   bool staged = true;
   const bool fixed = fixed_ok && mode == MODE_STEP && c.num_static == FIX_NS && c.num_dynamic == FIX_ND &&
-                     c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
+                     c.speed_x == 1 && c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX &&
+                     (int64_t)c.num_envs < FIX_MAX_ENVS;
   if (fixed && lanes10 == 2 && W == 10 && span_fits(W, c.radius_obstacle + c.radius_agent) &&
       (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
     // two lanes per env (step2_kernel): 32 envs per wave, 128 per block
@@ -3142,7 +3154,7 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lane
 Launch pick_rollout(const be_config& c, bool fixed_ok, int lpe5 = 0) {
   Launch L{nullptr, BLOCK_THREADS, 0, {0}};
   const bool fixed = fixed_ok && c.num_static == FIX_NS && c.num_dynamic == FIX_ND && c.speed_x == 1 &&
-                     c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
+                     c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX && (int64_t)c.num_envs < FIX_MAX_ENVS;
   if (fixed && c.window == 5 && (lpe5 == 4 || lpe5 == 8)) {   // small batches: L lanes per env, 32-env blocks
     L.fn = lpe5 == 8 ? rolloutw_kernel<5, FIX_NS, FIX_ND, 8> : rolloutw_kernel<5, FIX_NS, FIX_ND, 4>;
     L.epb = 32;
@@ -3165,7 +3177,7 @@ Launch pick_rollout(const be_config& c, bool fixed_ok, int lpe5 = 0) {
 Launch pick_policy_rollout(const be_config& c, bool fixed_ok, int HT, int KS, int NO) {
   Launch L{nullptr, BLOCK_THREADS, 0, {0}};
   const bool fixed = fixed_ok && c.num_static == FIX_NS && c.num_dynamic == FIX_ND && c.speed_x == 1 &&
-                     c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX;
+                     c.speed_y == 1 && c.radius_obstacle + c.radius_agent <= HW_MAX && (int64_t)c.num_envs < FIX_MAX_ENVS;
   if (fixed && c.window == 10 && HT == 13 && KS == 2 && NO == 10)
     L.fn = rollout_kernel<10, FIX_NS, FIX_ND, 13, 2, 10>;
   else if (fixed && c.window == 5 && HT == 8 && KS == 1 && NO == 10)

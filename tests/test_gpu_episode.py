@@ -555,3 +555,26 @@ def test_prev_dist_recompute_equals_read(gpu, monkeypatch):
         for e in envs:
             e.status()
             e.close()
+
+
+def test_fixed_kernels_batch_size_bound(gpu):
+    """The fixed-shape kernels address per-env arrays as a uniform base + a 32-bit byte offset, so the
+    dispatcher takes them only below 2^29 envs (FIX_MAX_ENVS: element i of an 8-byte array); at 2^29
+    the generic kernels (64-bit indexing) run.  Contexts only -- no state is allocated here."""
+    import ctypes as C
+    from gym_ballenv_amd import _abi
+    from gym_ballenv_amd.config import EnvConfig
+    lib = _abi.lib()
+    dev = torch.device(gpu).index or 0
+    names = {}
+    for n in ((1 << 29) - 1, 1 << 29):
+        cfg = EnvConfig().to_abi(n, 10)
+        ctx = C.c_void_p()
+        _abi.check(lib.be_create(C.byref(cfg), dev, C.byref(ctx)))
+        try:
+            names[n] = (lib.be_kernel_name(ctx, 0).decode(), lib.be_kernel_name(ctx, 2))   # rollout: NULL = loop
+        finally:
+            lib.be_destroy(ctx)
+    assert names[(1 << 29) - 1][0] == "be_kernel<10, 0, 13, 5>", names
+    assert names[1 << 29][0] == "be_kernel<10, 0, 0, 0>", names
+    assert names[1 << 29][1] is None or b"13, 5" not in names[1 << 29][1], names
