@@ -891,7 +891,8 @@ __device__ __forceinline__ double reset_dists(int32_t ag, int32_t go, int32_t a0
 template <int WT, int NSC, int NDC, int PMAX, class OSink, class ESink, int LPE = 1>
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
-                            uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl, OSink&& osink, ESink&& esink) {
+                            uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl, OSink&& osink, ESink&& esink,
+                            const uint64_t* span = nullptr) {   // span: the wave's row-span table (step2_kernel)
   // G + 1 lanes per env: lane k < G draws obstacle k, lane G the goal / agent block; every lane
   // runs ONE Philox chain, and the goal lane's four values reach the slot's lanes by readlane
   constexpr int K = Geo<WT>::K, G = NSC + NDC, GL = G + 1, P = (64 / GL < PMAX) ? 64 / GL : PMAX;
@@ -974,12 +975,19 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
       const int f = ox - (rax - WT / 2), e = oy - (ray - WT / 2);   // unit cell step (fixed-shape kernels)
       if ((uint32_t)(f + rx) <= (uint32_t)(WT - 1 + 2 * rx) && (uint32_t)(e + rx) <= (uint32_t)(K - 1 + 2 * rx)) {
         uint32_t mk[K];   // few lanes get here: the row masks branch-free, then same-address LDS atomics
+        if (span) {       // raster_rows_span's rows (window-relative f, e here)
+          const uint64_t* col = span + (e + rx);
+          const uint32_t sh = (uint32_t)(WT - 1 + rx - f);
 #pragma unroll
-        for (int r = 0; r < K; ++r) {
-          const int ady = abs(e - r);
-          const int hw = t.hw[min(ady, HW_MAX)];
-          const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
-          mk[r] = (ady <= rx && lo <= hi) ? (2u << hi) - (1u << lo) : 0u;
+          for (int r = 0; r < K; ++r) mk[r] = (uint32_t)(col[K - 1 - r] >> sh) & ((1u << WT) - 1u);
+        } else {
+#pragma unroll
+          for (int r = 0; r < K; ++r) {
+            const int ady = abs(e - r);
+            const int hw = t.hw[min(ady, HW_MAX)];
+            const int lo = max(f - hw, 0), hi = min(f + hw, WT - 1);
+            mk[r] = (ady <= rx && lo <= hi) ? (2u << hi) - (1u << lo) : 0u;
+          }
         }
 #pragma unroll
         for (int r = 0; r < K; ++r) atomicOr(&wrows[slot * K + r], mk[r]);
@@ -1952,10 +1960,10 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     };
     if (!(m & (m - 1)))
       wave_resets<WT, NSC, NDC, 1, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
-                                                                        nl.cnt, xrows, &s_rows[w][0], osink, esink);
+                                                                        nl.cnt, xrows, &s_rows[w][0], osink, esink, span);
     else
       wave_resets<WT, NSC, NDC, 64, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
-                                                                         nl.cnt, xrows, &s_rows[w][0], osink, esink);
+                                                                         nl.cnt, xrows, &s_rows[w][0], osink, esink, span);
   }
   DIAG(3);
   if (DBG(DBG_NO_OBS)) return;
