@@ -781,8 +781,9 @@ def moved(rf, B_eng, units, us, pmc, label="be_step_bytes (engine)"):
     return rf
 
 
-def board_roofline(B, N, us, pmc):
-    """HBM roofline of a createBoard kernel plus its newest committed counters: f64-VALU work, not HBM."""
+def board_roofline(B, N, us, pmc, steps_per_launch=1):
+    """HBM roofline of a createBoard kernel plus its newest committed counters: f64-VALU work, not HBM.
+    us is per step; a fused launch covers steps_per_launch steps, so its counters are scaled to one step."""
     ach = B * N / (us * 1e-6) / 1e9
     r = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
          "traffic": None,
@@ -790,6 +791,7 @@ def board_roofline(B, N, us, pmc):
                     "per env-step) at one wave per SIMD"}
     if pmc:
         ws = pmc["wave_cycle_split"]
+        pmc = dict(pmc, hbm_bytes_per_dispatch=pmc["hbm_bytes_per_dispatch"] / steps_per_launch)   # per step
         r.update({"traffic": pmc["hbm_bytes_per_dispatch"], "traffic_per_env_step": pmc["hbm_bytes_per_unit"],
                   "valu_insts_per_wave": pmc["per_wave"]["SQ_INSTS_VALU"],
                   "wave_cycle_split": ws, "pmc_source": pmc["source"],
@@ -865,7 +867,7 @@ def board_leg(args, gb, dev, rank, world, stream):
     res["fused"]["bytes_per_env_step"] = Bf
     res["fused"]["roofline"] = board_roofline(Bf, N, res["fused"]["kernel_us_per_step"],
                                               newest_pmc("pmc_board_rollout.json", "board_kernel<6, true",
-                                                            N * Kc))
+                                                            N * Kc), steps_per_launch=Kc)
     b.close()
     return res
 

@@ -27,8 +27,9 @@ by_grid = defaultdict(list)
 for r in csv.DictReader(open(a.trace)):
     t = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
     runs[r["Kernel_Name"]].append(t)
-    if "Grid_Size" in r:
-        by_grid[(r["Kernel_Name"], int(r["Grid_Size"]))].append(t)
+    g = r.get("Grid_Size", r.get("Grid_Size_X"))   # (counter CSVs: Grid_Size; kernel traces: Grid_Size_X)
+    if g:
+        by_grid[(r["Kernel_Name"], int(g))].append(t)
 for k in list(runs) + list(by_grid):
     (runs if k in runs else by_grid)[k].sort()
 
