@@ -2912,13 +2912,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     u4 b1{0u, 0u, 0u, 0u};
     if (NDC > 5) b1 = philox(gid, episode, (uint32_t)len, tag(PURPOSE_STEP_OBS, 1u), p.seed);
     const v2s agv = __builtin_bit_cast(v2s, pk(ax, ay));
+    uint32_t* nlp = nl.base;   // (step2_kernel's saturating slot advance; nl.cnt set after the tests)
     auto obstacle_pk = [&](int32_t opk, bool& hit) {   // be_kernel's packed int16x2 test
       const v2s d = __builtin_elementwise_sub_sat(__builtin_bit_cast(v2s, opk), agv);
       hit |= (uint32_t)__builtin_amdgcn_sdot2(d, d, 0, false) <= R2;
       const v2u b = __builtin_bit_cast(v2u, __builtin_elementwise_add_sat(d, boxo));
       const v2u over = __builtin_elementwise_sub_sat(b, boxw);
-      nl.base[nl.cnt * BLOCK_THREADS] = __builtin_bit_cast(uint32_t, d);
-      nl.cnt += __builtin_bit_cast(uint32_t, over) == 0u ? 1 : 0;
+      *nlp = __builtin_bit_cast(uint32_t, d);
+      nlp += BLOCK_THREADS * __builtin_elementwise_sub_sat(1u, __builtin_bit_cast(uint32_t, over));
     };
 #pragma unroll
     for (int j = 0; j < NDC; ++j) {
@@ -2930,6 +2931,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void rollout_kernel(KParams p) {
     }
 #pragma unroll
     for (int j = 0; j < NSC; ++j) obstacle_pk(so[j], hs);
+    nl.cnt = (int)(lds_bytes(nl.base, nlp) / (BLOCK_THREADS * 4u));
 
     // ---- distance, reward, done (ballenv_env.py:268-286, 200-229)
     // (computing this right after the move, as step2_kernel does, measured slower here)
