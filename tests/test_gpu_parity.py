@@ -327,6 +327,47 @@ def test_goal_threshold_boundaries(gpu, W):
         env.close()
 
 
+@pytest.mark.parametrize("W", [10, 5])
+def test_reset_rejection_limit(gpu, W):
+    """A 20 x 30 field where no spawn passes the reset's rejection tests: every static obstacle overlaps
+    the agent's or the goal's rectangle (ballenv_env.py:131-149, :193-197) and no goal is 50 px from
+    the agent (:121-126), so every loop stops at its 4 096-draw bound.  be_reset (the block-cooperative
+    reset) and the fixed-shape step kernels' autoreset (wave_resets; a collision every step) leave the
+    oracle's state bit for bit -- the same last draws -- and status() reports the bound."""
+    from gym_ballenv_amd._abi import BallEnvError
+    from gym_ballenv_amd.config import EnvConfig
+    N, T, seed = 200, 4, 5
+    cfg_py = EnvConfig(screen_width=20, screen_height=30, strip_obs_y=5, strip_goal_x=20, strip_agent_x=20,
+                       time_limit=3)
+    env = make_env(cfg_py, N, W, gpu, seed=seed)
+    assert env.kernel_name("step") in ("step2_kernel<10, 13, 5>", "stepw_kernel<5, 13, 5, 8>", f"be_kernel<{W}, 0, 13, 5>")
+    cfg = cfg_py.to_abi(N, W, seed=seed)
+    st, out = oracle.new_state(cfg), oracle.new_out(cfg)
+    env.reset()
+    assert oracle.reset(cfg, st, out) & 2
+    with pytest.raises(BallEnvError, match="reset rejection limit"):
+        env.status()
+    assert_state_equal(env, st, "reset")
+    acts = env.sample_actions(T, seed=seed)
+    resets = 0
+    for t in range(T):
+        obs, reward, done, _ = env.step(acts[t])
+        status = oracle.step(cfg, st, out, actions=acts[t].cpu().numpy())
+        np.testing.assert_array_equal(obs.cpu().numpy(), out["obs"], err_msg=f"t={t} obs")
+        np.testing.assert_array_equal(reward.cpu().numpy(), out["reward"], err_msg=f"t={t} reward")
+        np.testing.assert_array_equal(done.cpu().numpy(), out["done"], err_msg=f"t={t} done")
+        assert_state_equal(env, st, f"t={t}")
+        resets += int(out["done"].sum())
+        assert bool(status & 2) == bool(out["done"].any())   # every reset here hits the bound
+        if status & 2:
+            with pytest.raises(BallEnvError, match="reset rejection limit"):
+                env.status()
+        else:
+            env.status()
+    assert resets >= N   # (the TimeLimit alone ends every episode by step 3)
+    env.close()
+
+
 def test_large_batch_subset_vs_oracle(gpu):
     """2^20 envs (past the Infinity Cache): a contiguous slice matches the oracle run
     on just that slice (Philox streams are keyed by global env id)."""

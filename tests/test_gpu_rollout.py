@@ -17,8 +17,9 @@ from test_gpu_parity import KEYS, make_env, np_state
 pytestmark = pytest.mark.gpu
 
 
-def _run_pair(cfg_py, N, W, K, chunks, seed=7, terminal=False, lens=None):
-    """Env A: K be_step calls.  Env B: be_rollout over `chunks` (step counts summing to K)."""
+def _run_pair(cfg_py, N, W, K, chunks, seed=7, terminal=False, lens=None, status=None):
+    """Env A: K be_step calls.  Env B: be_rollout over `chunks` (step counts summing to K).  status: the
+    device-status text both envs must report at the end (None: no status bit)."""
     a, b = (make_env(cfg_py, N, W, "cuda:0", seed=seed, terminal_obs=terminal) for _ in range(2))
     acts = a.sample_actions(K, seed=seed + 1)
     a.reset()
@@ -56,8 +57,13 @@ def _run_pair(cfg_py, N, W, K, chunks, seed=7, terminal=False, lens=None):
     for k in KEYS:
         np.testing.assert_array_equal(sb[k], sa[k], err_msg=f"final state[{k}]")
     np.testing.assert_array_equal(b.stats_buf.cpu().numpy(), a.stats_buf.cpu().numpy())
-    a.status()
-    b.status()
+    for e in (a, b):
+        if status is None:
+            e.status()
+        else:
+            from gym_ballenv_amd._abi import BallEnvError
+            with pytest.raises(BallEnvError, match=status):
+                e.status()
     n_done = int(ref["done"].sum())
     a.close()
     b.close()
@@ -242,6 +248,21 @@ def test_w5_small_batch_kernels_non_default_radius(gpu, r_obs, monkeypatch):
     monkeypatch.setenv("BALLENV_STEP5_LPE", "8")
     monkeypatch.setenv("BALLENV_ROLLOUT5_LPE", "1")
     _run_pair(cfg, 4096, 5, 40, (40,), terminal=True)                # one-lane rollout vs stepw steps
+
+
+@pytest.mark.parametrize("W,lpe", [(10, "1"), (5, "8")])
+def test_fused_rollouts_rejection_limit(gpu, W, lpe, monkeypatch):
+    """The fused rollouts' autoreset (wave_resets in rollout_kernel / rolloutw_kernel) on the 20 x 30
+    field of test_gpu_parity.py::test_reset_rejection_limit, where every reset loop stops at its
+    4 096-draw bound and every env resets every step: bit for bit the step path's trajectory, and both
+    report the bound."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg = EnvConfig(screen_width=20, screen_height=30, strip_obs_y=5, strip_goal_x=20, strip_agent_x=20, time_limit=3)
+    monkeypatch.setenv("BALLENV_ROLLOUT5_LPE", lpe)
+    e = make_env(cfg, 256, W, gpu, seed=3)
+    assert e.kernel_name("rollout") == ("rollout_kernel<10, 13, 5, 0, 1, 10>" if W == 10 else "rolloutw_kernel<5, 13, 5, 8>")
+    e.close()
+    _run_pair(cfg, 256, W, 6, (2, 4), terminal=True, status="reset rejection limit")
 
 
 @pytest.mark.parametrize("r_obs", [21, 58])
