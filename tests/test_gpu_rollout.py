@@ -109,8 +109,9 @@ def test_rollout_errors(gpu):
     env.close()
 
 
-def _policy_pair(cfg_py, N, W, T, chunk, record, policy=None, horizons=2, seed=11):
-    """Rollout(backend="hip") (two launches per step) vs Rollout(backend="fused") (be_policy_rollout)."""
+def _policy_pair(cfg_py, N, W, T, chunk, record, policy=None, horizons=2, seed=11, status=None):
+    """Rollout(backend="hip") (two launches per step) vs Rollout(backend="fused") (be_policy_rollout).
+    status: the device-status text both envs must report at the end (None: no status bit)."""
     from gym_ballenv_amd.policy import Policy, reference_weights
     from gym_ballenv_amd.rollout import Rollout
     if policy is None:
@@ -139,7 +140,12 @@ def _policy_pair(cfg_py, N, W, T, chunk, record, policy=None, horizons=2, seed=1
     n_done = int(ros[0].dones.sum())
     lit = int((ros[0].obs[:, :, 4:].amax(-1) > 0).sum()) if record else -1
     for r, e in zip(ros, envs):
-        e.status()
+        if status is None:
+            e.status()
+        else:
+            from gym_ballenv_amd._abi import BallEnvError
+            with pytest.raises(BallEnvError, match=status):
+                e.status()
         r.close()
         e.close()
     return n_done, lit
@@ -254,8 +260,8 @@ def test_w5_small_batch_kernels_non_default_radius(gpu, r_obs, monkeypatch):
 def test_fused_rollouts_rejection_limit(gpu, W, lpe, monkeypatch):
     """The fused rollouts' autoreset (wave_resets in rollout_kernel / rolloutw_kernel) on the 20 x 30
     field of test_gpu_parity.py::test_reset_rejection_limit, where every reset loop stops at its
-    4 096-draw bound and every env resets every step: bit for bit the step path's trajectory, and both
-    report the bound."""
+    4 096-draw bound and every env resets every step: bit for bit the step path's trajectory (and, at
+    W=10, the fused policy rollout its two-launch loop's), and both report the bound."""
     from gym_ballenv_amd.config import EnvConfig
     cfg = EnvConfig(screen_width=20, screen_height=30, strip_obs_y=5, strip_goal_x=20, strip_agent_x=20, time_limit=3)
     monkeypatch.setenv("BALLENV_ROLLOUT5_LPE", lpe)
@@ -263,6 +269,9 @@ def test_fused_rollouts_rejection_limit(gpu, W, lpe, monkeypatch):
     assert e.kernel_name("rollout") == ("rollout_kernel<10, 13, 5, 0, 1, 10>" if W == 10 else "rolloutw_kernel<5, 13, 5, 8>")
     e.close()
     _run_pair(cfg, 256, W, 6, (2, 4), terminal=True, status="reset rejection limit")
+    if W == 10:   # the config-5 fused policy rollout's autoreset (be_policy_rollout) against its two-launch loop
+        n_done, _ = _policy_pair(cfg, 256, W, 6, 3, False, horizons=1, status="reset rejection limit")
+        assert n_done == 256 * 6
 
 
 @pytest.mark.parametrize("r_obs", [21, 58])
