@@ -347,13 +347,13 @@ def test_step_kernel_dispatch_by_batch(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("N,tl,f32", [(20000, 20, False), (65536, 1000, False), (1000, 7, False), (4000, 20, True),
-                                     (32768, 1000, False)])
+                                     (32768, 1000, False), (1, 7, False), (33, 7, True)])
 def test_step2_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
     """step2_kernel (two lanes per env) equals the one-lane fixed-shape kernel bit for bit --
     obs, reward, done, truncated, final return / length, terminal obs, the state and the
     stats slots -- through mass truncation (tl=20: every env of every wave resets on the same
     steps) and at the defaults from random episode phases (N=32768: config 4's per-GPU shard at
-    8 GPUs); N=20000 / 1000 leave partial blocks."""
+    8 GPUs); N=20000 / 1000 leave partial blocks, N=1 / 33 a lone env and a one-env last wave."""
     from gym_ballenv_amd.config import EnvConfig
     cfg_py = EnvConfig(time_limit=tl)
     W = 10
