@@ -450,13 +450,15 @@ def test_step_n_equals_step_calls(gpu):
         e.close()
 
 
-@pytest.mark.parametrize("N,tl,f32", [(4096, 1000, False), (4096, 20, False), (1000, 7, True), (20000, 20, False)])
+@pytest.mark.parametrize("N,tl,f32", [(4096, 1000, False), (4096, 20, False), (1000, 7, True), (20000, 20, False),
+                                     (1, 7, False), (33, 7, True)])
 def test_stepw_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
     """stepw_kernel (W=5, 8 and 4 lanes per env, 32-env blocks with a last-wave stats fold) equals
     the one-lane fixed-shape kernel bit for bit -- obs (u8 and f32), reward, done, truncated,
     final return / length, terminal obs, the state and the stats slots -- through mass truncation
     (tl=20 / 7: every env of every wave resets on the same steps) and at the defaults from random
-    episode phases; N=1000 / 20000 leave partial blocks and a partial last wave."""
+    episode phases; N=1000 / 20000 leave partial blocks and a partial last wave, N=1 / 33 a lone env and a
+    one-env last block."""
     from gym_ballenv_amd.config import EnvConfig
     cfg_py = EnvConfig(time_limit=tl)
     W = 5
