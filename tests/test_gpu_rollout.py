@@ -256,6 +256,26 @@ def test_w5_small_batch_kernels_non_default_radius(gpu, r_obs, monkeypatch):
     _run_pair(cfg, 4096, 5, 40, (40,), terminal=True)                # one-lane rollout vs stepw steps
 
 
+@pytest.mark.parametrize("W,lpe,N", [(10, "1", 2), (10, "1", 34), (5, "8", 16), (5, "8", 48)])
+def test_fused_rollouts_tiny_batches(gpu, W, lpe, N, monkeypatch):
+    """The fused rollouts at the smallest batches they take -- be_rollout writes whole 16-byte obs
+    words, so N * (4 + W^2) % 16 == 0: N = 2 / 16 -- and one block past them (N = 34 / 48), through
+    TimeLimit resets (tl=7) and chunks that cross them, against the step path (rollout_kernel at W=10,
+    rolloutw_kernel at W=5); a batch off that grid is refused, not padded."""
+    from gym_ballenv_amd._abi import BallEnvError
+    from gym_ballenv_amd.config import EnvConfig
+    cfg = EnvConfig(time_limit=7)
+    monkeypatch.setenv("BALLENV_ROLLOUT5_LPE", lpe)
+    e = make_env(cfg, N, W, gpu, seed=3)
+    assert e.kernel_name("rollout") == ("rollout_kernel<10, 13, 5, 0, 1, 10>" if W == 10 else "rolloutw_kernel<5, 13, 5, 8>")
+    e.close()
+    _run_pair(cfg, N, W, 20, (3, 9, 8), terminal=True)
+    bad = make_env(cfg, N - 1, W, gpu, seed=3)
+    with pytest.raises(BallEnvError, match="16-byte aligned"):
+        bad.rollout(bad.sample_actions(2, seed=1))
+    bad.close()
+
+
 @pytest.mark.parametrize("W,lpe", [(10, "1"), (5, "8")])
 def test_fused_rollouts_rejection_limit(gpu, W, lpe, monkeypatch):
     """The fused rollouts' autoreset (wave_resets in rollout_kernel / rolloutw_kernel) on the 20 x 30
