@@ -38,6 +38,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 DIST_ON = False         # a torch.distributed process group is up (any launch under torchrun, even 1 rank)
+LAST_OWN_ELAPSED = 0.0  # timed_graph_steps: this rank's own wall time of its last timed region
 
 
 def parse():
@@ -216,6 +217,8 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    global LAST_OWN_ELAPSED
+    LAST_OWN_ELAPSED = el       # this rank's own wall time (the per-rank rows of graph_steps_leg)
     if DIST_ON:
         dist.barrier()
     if DIST_ON:
@@ -223,6 +226,19 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el, ev0.elapsed_time(ev1) / steps
+
+
+def rank_rows(dev, row):
+    """Per-rank diagnostics of a timed region at N > 1 (the row of every rank, all_gather_object):
+    a scaling run then explains its own curve -- which rank / GPU was slow, by how much, and what
+    the stats exchange cost."""
+    import torch
+    import torch.distributed as dist
+    row = dict(row, rank=dist.get_rank(), host=os.uname().nodename,
+               device_uuid=str(torch.cuda.get_device_properties(dev).uuid))
+    rows = [None] * dist.get_world_size()
+    dist.all_gather_object(rows, row)
+    return rows
 
 
 def cold_actions_leg(args, env, lib, dev, stream, world, B):
@@ -415,17 +431,24 @@ def policy_roofline(args, gb, dev, rank, pol, us_per_step, chunk, img):
     return res
 
 
-def rollout_leg(args, gb, dev, rank, world, stream):
+def rollout_leg(args, gb, dev, rank, world, stream, N=None, W=None, env_offset=None,
+                pmc_suffix="pmc_rollout_kernel.json", label=None):
     """SURVEY 8(d) fused multi-step mode: the same random-action rollout as the headline, but
     be_rollout runs --rollout-chunk steps per launch with each env's state in registers
     (bit-identical outputs to be_step, tests/test_gpu_rollout.py).  Per step it writes the
-    obs row, reward, done and truncated of every env into (K, N, ...) trajectory buffers."""
+    obs row, reward, done and truncated of every env into (K, N, ...) trajectory buffers.
+    N / W / env_offset: another BASELINE size of the same mode (config 2's 4 096 envs at W=5:
+    rolloutw_kernel; config 4's 32 768-env shard at the last rank's ids); pmc_suffix names its
+    committed counter profile (profiles/rNN_<suffix>)."""
     import ctypes as C
     import torch
     from gym_ballenv_amd import _abi
-    N, W, T, Kc = args.envs, args.window, args.rollout_steps, max(1, min(args.rollout_chunk, args.rollout_steps))
+    N = args.envs if N is None else N
+    W = args.window if W is None else W
+    T, Kc = args.rollout_steps, max(1, min(args.rollout_chunk, args.rollout_steps))
     T -= T % Kc
-    env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=rank * N)
+    off = rank * N if env_offset is None else env_offset
+    env = gb.BatchedBallEnv(N, W, gb.EnvConfig(), device=dev, seed=0xBA11, env_offset=off)
     acts = env.sample_actions(T, seed=0xBA11)
     env.reset()
     env.rollout(acts[:Kc])                    # warm-up launch; allocates the (Kc, N, ...) buffers
@@ -462,8 +485,10 @@ def rollout_leg(args, gb, dev, rank, world, stream):
     B_io = 1 + 8 + 1 + 1 + 4 + W * W
     B_state = gb.step_bytes(gb.EnvConfig(), W) - (1 + 8 + 1 + 4 + W * W)
     B = B_io + B_state / Kc
-    res = {"workload": f"random-action rollout, {N} envs/GPU, W={W}, be_rollout {Kc} steps per launch "
+    res = {"workload": (label or f"random-action rollout, {N} envs/GPU, W={W}") +
+                       f", be_rollout {Kc} steps per launch "
                        "(state in registers; per-step obs/reward/done/truncated to (K, N, ...) buffers)",
+           "envs": N, "window": W, "env_offset": off, "steps_per_launch": Kc,
            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
            "kernel_us_per_step": us_step, "bytes_per_env_step": B,
            "achieved_GBs": B * N / (us_step * 1e-6) / 1e9,
@@ -472,9 +497,10 @@ def rollout_leg(args, gb, dev, rank, world, stream):
     # when they were taken on the kernel this run launched)
     kname = env.kernel_name("rollout")
     res["kernel"] = kname
-    d = newest_pmc("pmc_rollout_kernel.json", f"::{kname}(", N * Kc)
+    d = newest_pmc(pmc_suffix, f"::{kname}(", N * Kc)
     if d:
-        res.update({"traffic_per_env_step": d["hbm_bytes_per_unit"], "traffic_source": d["source"]})
+        res.update({"traffic_per_env_step": d["hbm_bytes_per_unit"], "traffic_source": d["source"],
+                    "measured_frac": d["hbm_bytes_per_dispatch"] / (us_step * Kc * 1e-6) / 1e9 / HBM_PEAK_GBS})
     moved(res, B, N * Kc, us_step * Kc, d, "algorithmic (above)")
     env.close()
     return res
@@ -521,12 +547,19 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
     env.clear_stats()    # in place (the graphs' stats pointer): episodes of the timed steps only
     torch.cuda.synchronize(dev)
     el, ms = timed_graph_steps(graphs, T, dev, stream, world)
+    own_el = LAST_OWN_ELAPSED
     env.status()
     kname = env.kernel_name("step")
-    episodes = None
+    episodes = rows = None
     if global_envs is not None:
+        t_ag = time.perf_counter()
         per_rank = gb.gather_stats(env.stats_record()) if DIST_ON else env.stats_record().reshape(1, -1)
+        torch.cuda.synchronize(dev)
+        ag_us = (time.perf_counter() - t_ag) * 1e6
         episodes = gb.combine_stats(per_rank)
+        if DIST_ON and world > 1:
+            rows = rank_rows(dev, {"envs": N, "env_offset": off, "kernel": kname, "kernel_us_mean": ms * 1e3,
+                                   "ms_per_step": own_el / T * 1e3, "stats_all_gather_us": ag_us})
     del graphs
     env.close()
     B = gb.survey_step_bytes(cfg, W)
@@ -544,6 +577,8 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
     moved(res["roofline"], B_eng, N, us, None)    # legs with a committed profile re-run it (add_measured)
     if episodes is not None:
         res["episodes"] = episodes
+    if rows is not None:
+        res["per_rank"] = rows
     return res, kname
 
 
@@ -995,24 +1030,29 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize(dev)   # (measured: a spin on the end event first adds ~1.5 us, tools/sync_cost.py)
     elapsed = time.perf_counter() - t0
+    own_elapsed = elapsed
+    # average launch duration over the timed region (events on the launch stream)
+    kern_ms = ev0.elapsed_time(ev1) / K
     if DIST_ON:
         dist.barrier()
     n_devices = 1
+    per_rank_rows = None
     if DIST_ON:
         el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         elapsed = float(el.item())
+        t_ag = time.perf_counter()
         per_rank = gb.gather_stats(env.stats_record())            # RCCL all_gather of episode returns
+        torch.cuda.synchronize(dev)
+        ag_us = (time.perf_counter() - t_ag) * 1e6
         ep = gb.combine_stats(per_rank)
-        devs = [None] * world                                      # distinct GPUs, not ranks (gloo rehearsal)
-        dist.all_gather_object(devs, (os.uname().nodename, str(torch.cuda.get_device_properties(dev).uuid)))
-        n_devices = len(set(devs))
+        per_rank_rows = rank_rows(dev, {"local_rank": local_rank, "envs": N, "env_offset": rank * N,
+                                        "kernel_us_mean": kern_ms * 1e3, "ms_per_step": own_elapsed / K * 1e3,
+                                        "stats_all_gather_us": ag_us})
+        n_devices = len({(r["host"], r["device_uuid"]) for r in per_rank_rows})   # distinct GPUs, not ranks
     else:
         ep = env.episode_stats()
     env.status()
-
-    # average launch duration over the timed region (events on the launch stream)
-    kern_ms = ev0.elapsed_time(ev1) / K
 
     total_steps = K * N * world
     value = total_steps / elapsed
@@ -1037,6 +1077,25 @@ def main():
     if board_res is not None:
         board_res["cpu_baseline"] = board_base
     roll_res = rollout_leg(args, gb, dev, rank, world, stream) if args.rollout_steps > 0 else None
+    if roll_res is not None and world == 1:
+        # the same fused mode at the other BASELINE sizes (SURVEY 8(d) reports it separately): config 2
+        # (4 096 envs, W=5: rolloutw_kernel) and config 4's 8-GPU shard (32 768 envs at the last rank's ids)
+        from gym_ballenv_amd.distributed import shard
+        roll_res["config2"] = rollout_leg(args, gb, dev, 0, 1, stream, N=args.config2_envs, W=5, env_offset=0,
+                                          pmc_suffix="pmc_rollout_config2.json",
+                                          label=f"BASELINE config 2: random-action rollout, {args.config2_envs} envs, W=5")
+        off8, n8 = shard(args.config4_envs, 7, 8)
+        roll_res["shard_32768"] = rollout_leg(args, gb, dev, 0, 1, stream, N=n8, W=10, env_offset=off8,
+                                              pmc_suffix=f"pmc_rollout_shard_{n8}.json",
+                                              label=f"config 4's 8-GPU shard: random-action rollout, {n8} envs "
+                                                    f"(global ids {off8}..{off8 + n8 - 1}), W=10")
+        if base is not None:   # the host port at the same windows (cpu_baseline.by_window)
+            for key, w in (("config2", 5), ("shard_32768", 10)):
+                bw = base["by_window"].get(f"W={w}")
+                if bw:
+                    roll_res[key]["cpu_baseline_ref"] = {"window": w, "aggregate": bw["aggregate"],
+                                                         "per_core": bw["per_core_mean"], "cores": base["cores"],
+                                                         "source": f"cpu_baseline.by_window.W={w}"}
     blocks_res = blocks_leg(args, gb, dev, rank, world, stream) if args.blocks_launches > 0 else None
 
     if rank == 0:
@@ -1078,6 +1137,12 @@ def main():
         }
         moved(line["roofline"], B_eng, N, kern_ms * 1e3, pmc)
         line["episodes_note"] = "episodes finished during the timed steps (all ranks)"
+        if per_rank_rows is not None:
+            # N > 1: each rank's own timing (the line's ms_per_step is the max of these), its GPU, and
+            # the stats all_gather's wall time -- a scaling run explains its own curve
+            line["per_rank"] = per_rank_rows
+            line["dist_backend"] = args.dist_backend
+            line["rccl_world_size"] = dist.get_world_size() if args.dist_backend == "nccl" else None
         print(json.dumps(line), flush=True)
     env.close()
     if DIST_ON:

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_STATIC, MAX_DYNAMIC, MAX_GOALS, MAX_ACTIONS, MAX_WINDOW = 64, 32, 16, 16, 64
 
 BE_OK, BE_E_INVALID, BE_E_HIP, BE_E_NOMEM, BE_E_DEVICE = 0, -1, -2, -3, -4
@@ -25,7 +25,8 @@ LIB_PATH = os.environ.get("BALLENV_LIB") or os.path.join(os.path.dirname(os.path
 EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_bytes", "be_stats_slots",
            "be_last_error", "be_kernel_name",
            "be_create", "be_destroy", "be_reset", "be_step", "be_step_n", "be_rollout", "be_observe", "be_sample_actions",
-           "be_status", "be_state_blob_bytes", "be_save_state", "be_load_state", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
+           "be_status", "be_state_blob_bytes", "be_save_state", "be_load_state",
+           "be_pool_fill", "be_pool_invalidate", "be_pool_set_period", "be_pool_bytes", "be_pool_entry", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
            "be_policy_rollout", "be_policy_bytes", "be_observe_blocks",
            "be_board_config_default", "be_board_create", "be_board_destroy", "be_board_last_error",
            "be_board_reset", "be_board_step", "be_board_rollout", "be_board_observe", "be_board_status")
@@ -130,6 +131,11 @@ def lib() -> C.CDLL:
         "be_state_blob_bytes": (i64, [P(BeConfig)]),
         "be_save_state": (C.c_int, [vp, P(BeState), vp, vp]),
         "be_load_state": (C.c_int, [vp, P(BeState), vp, vp]),
+        "be_pool_fill": (C.c_int, [vp, P(BeState), vp]),
+        "be_pool_invalidate": (C.c_int, [vp, vp]),
+        "be_pool_set_period": (C.c_int, [vp, i32]),
+        "be_pool_bytes": (i64, [vp]),
+        "be_pool_entry": (C.c_int, [vp, i32, i32, P(C.c_uint32), P(C.c_double), i32]),
         "be_policy_create": (C.c_int, [vp, i32, i32, P(vp)]),
         "be_policy_destroy": (C.c_int, [vp]),
         "be_policy_load": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
@@ -147,11 +153,18 @@ def lib() -> C.CDLL:
         "be_board_observe": (C.c_int, [vp, P(BeBoardState), P(BeBoardOut), vp]),
         "be_board_status": (C.c_int, [vp, P(i32), vp]),
     }
+    # a BALLENV_LIB diagnostics build from an earlier commit (tools/build_rev_lib.sh, A/B runs) may
+    # predate the newest entry points and ABI version; the in-tree library must match exactly
+    diag = bool(os.environ.get("BALLENV_LIB"))
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None and diag and name.startswith("be_pool_"):
+            continue
+        if fn is None:
+            raise BallEnvError(f"{LIB_PATH} does not export {name}: rebuild it")
         fn.restype, fn.argtypes = res, args
     v = L.be_abi_version()
-    if v != ABI_VERSION:
+    if v != ABI_VERSION and not (diag and v >= 6):
         raise BallEnvError(f"{LIB_PATH} has ABI {v}, expected {ABI_VERSION}: rebuild it")
     _lib = L
     return L

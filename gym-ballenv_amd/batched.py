@@ -112,10 +112,18 @@ class BatchedBallEnv:
         _abi.check(self._lib.be_create(C.byref(self._abi_cfg), dev, C.byref(ctx)))
         self._ctx = ctx
         self._dev_index = dev
+        # the raw current-stream getter saves host time per step(); it is private torch API, so a
+        # torch without it falls back to the public Stream object (same handle, a little slower)
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        if raw is not None:
+            self._stream = lambda: C.c_void_p(raw(dev))
+        else:
+            self._stream = lambda: C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
     def _stream(self):
-        """The caller's current stream on this env's device (raw handle; no Stream object)."""
-        return C.c_void_p(torch._C._cuda_getCurrentRawStream(self._dev_index))
+        """The caller's current stream on this env's device (raw handle; replaced per instance in
+        _create_ctx by the fastest getter this torch has)."""
+        return C.c_void_p(torch.cuda.current_stream(self._dev_index).cuda_stream)
 
     # ------------------------------------------------------------------ gym surface
     @property
@@ -158,7 +166,7 @@ class BatchedBallEnv:
         return self.obs_f32 if self._want_f32 else self.obs
 
     def step(self, actions: Optional[torch.Tensor] = None, deltas: Optional[torch.Tensor] = None,
-             draw_tape: Optional[torch.Tensor] = None):
+             draw_tape: Optional[torch.Tensor] = None, copy: bool = False):
         """One step of every env.
 
         actions: (N,) integer indices into ``cfg.actions`` (the move_list of
@@ -166,7 +174,16 @@ class BatchedBallEnv:
         neither: uniformly sampled actions (Philox, keyed by global env id).
         draw_tape: (Nd, 2, N) int16 obstacle-move randint values (parity mode).
         Returns (obs, reward f64, done bool, info).
+
+        Return semantics: with ``copy=False`` (the default, no allocation per step) obs, reward,
+        done and the info tensors are the env's output buffers, overwritten by the NEXT step --
+        a caller that keeps per-step outputs (``rewards.append(reward)``, ball_cnn_ac3.py:610)
+        must ``.clone()`` them.  ``copy=True`` returns fresh tensors each call, as
+        BallEnv.step returns a fresh np.array and float (ballenv_env.py:289).
         """
+        if copy:
+            obs, reward, done, info = self.step(actions, deltas, draw_tape)
+            return obs.clone(), reward.clone(), done.clone(), {k: v.clone() for k, v in info.items()}
         if actions is not None and deltas is None and draw_tape is None:
             # the common call (ball_cnn_ac3.py:588 for every env): the same (N,) u8 action buffer
             # each step skips the re-checks -- one ctypes call, the info dict prebuilt (the host
@@ -300,6 +317,38 @@ class BatchedBallEnv:
         ids = {"step": 0, "step_sampled": 1, "rollout": 2, "reset": 3, "observe": 4}
         r = self._lib.be_kernel_name(self._ctx, ids[entry])
         return r.decode() if r else None
+
+    # ------------------------------------------------------------------ the autoreset pool
+    # (include/ballenv.h: precomputed next-episode resets the fixed-shape step kernels copy on done;
+    # results are bit-identical with or without it -- these calls change timing only)
+    def pool_bytes(self) -> int:
+        """Device bytes of this env's autoreset pool (0: its step kernel draws every reset inline)."""
+        return int(self._lib.be_pool_bytes(self._ctx))
+
+    def pool_fill(self) -> None:
+        """Draw every env's stale entries now (be_pool_fill), on the current stream."""
+        _abi.check(self._lib.be_pool_fill(self._ctx, C.byref(self._st), self._stream()), self._ctx)
+
+    def pool_invalidate(self) -> None:
+        """Mark every entry unwritten: resets are drawn inline until the next fill."""
+        _abi.check(self._lib.be_pool_invalidate(self._ctx, self._stream()), self._ctx)
+
+    def pool_set_period(self, period: int) -> None:
+        """be_step queues a fill every ``period`` steps (0: only reset / load_state / pool_fill)."""
+        _abi.check(self._lib.be_pool_set_period(self._ctx, int(period)), self._ctx)
+
+    def pool_entry(self, env: int, slot: int, write=None):
+        """Test hook: (words u32 (6 + Ns + Nd,), f64 (2,)) of env's entry in slot (episode & 1), or
+        overwrite it with ``write = (words, f64)``.  Synchronises the device."""
+        nw = 6 + self.cfg.num_static + self.cfg.num_dynamic
+        w, d = (C.c_uint32 * nw)(), (C.c_double * 2)()
+        if write is not None:
+            for k, v in enumerate(write[0]):
+                w[k] = int(v) & 0xFFFFFFFF
+            d[0], d[1] = float(write[1][0]), float(write[1][1])
+        _abi.check(self._lib.be_pool_entry(self._ctx, int(env), int(slot), w, d, 1 if write is not None else 0),
+                   self._ctx)
+        return list(w), list(d)
 
     # ------------------------------------------------------------------ bookkeeping
     def status(self) -> int:

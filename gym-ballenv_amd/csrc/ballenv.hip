@@ -129,7 +129,64 @@ struct KParams {
   uint8_t* obs_last;           // (N, F) obs after the last step, or NULL
   uint8_t* act_out; float* logp_out; float* value_out;   // (steps, N)
   unsigned long long pol_seed;
+  // the autoreset pool (layout below; nullptr: every reset is drawn inline)
+  uint32_t* pool;
 };
+
+// ------------------------------------------------------------------ the autoreset pool
+// A reset in Philox mode is a pure function of (seed, global env id, new episode) and the context's
+// config (reset_env_philox's counter layout), so it can be drawn before the env finishes.
+// pool_fill_kernel draws, for every env at episode e, the resets into episodes e+1 and e+2; the step
+// kernels (step2_kernel, stepw_kernel) copy the entry of episode e+1 when the env finishes, instead
+// of running the reset's Philox chains on the wave's critical path, and fall back to the inline
+// wave_resets pass when the entry is stale (its tag is not e+1: the env reset twice since the last
+// fill, or no fill ran).  Two entries per env, slot = episode & 1 (entry index x = slot * N + env),
+// everything addressed from the one base p.pool (a uniform pointer + a 32-bit byte offset + an
+// immediate: no per-array base pointers to keep in SGPRs):
+//   tags    uint2 [2N] at byte 0:      (the episode the entry resets into, flags: POOL_VALID written,
+//                                      POOL_REJ a rejection loop hit its bound) -- the fill's scan
+//                                      reads these 8 bytes per entry, coalesced
+//   bodies  112 B [2N] at byte 16 N:   the entry itself, contiguous (a consuming lane reads it with
+//                                      seven 16-byte loads):
+//     w0..2  ROWS: the reset obs's distinct window rows, packed as the consuming kernel ORs them
+//            (W = 10: three rows per word at bits 10 r; W = 5: four rows at bits 5 r, in w0)
+//     w3 AGENT, w4 GOAL (packed xy), w5 unused, w6..7 PREV f64 (state[2], the pre-resample distance,
+//     Q9), w8..9 TOTAL f64, w10.. the NS statics' then the ND dynamics' packed xy (a reset's dyn_goal
+//     is k)
+constexpr uint32_t POOL_VALID = 1u, POOL_REJ = 2u;
+constexpr int PB_ROWS = 0, PB_AGENT = 3, PB_GOAL = 4, PB_PREV = 6, PB_TOTAL = 8, PB_OBS = 10;
+__host__ __device__ constexpr int pool_body_words(int ns, int nd) { return (PB_OBS + ns + nd + 3) & ~3; }
+__host__ __device__ constexpr int64_t pool_bytes_per_env(int ns, int nd) { return 2 * (8 + 4ll * pool_body_words(ns, nd)); }
+static_assert(pool_body_words(13, 5) == 28, "the fixed-shape kernels' 112-byte entry body");
+// byte offset of word w of entry x's body (N <= 2^22 keeps every offset below 2^32: pool_max_envs)
+__device__ __forceinline__ uint32_t pool_body(uint32_t n, uint32_t x, int nbw) { return 16u * n + x * (4u * (uint32_t)nbw); }
+// T at byte off + imm of the pool: the uniform base + zext(32-bit offset) + an immediate, so the
+// access is one global load / store with the immediate in its offset field
+template <class T>
+__device__ __forceinline__ T pool_ld(const uint32_t* pool, uint32_t off, uint32_t imm = 0) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(pool) + (size_t)off + imm);
+}
+template <class T>
+__device__ __forceinline__ void pool_st(uint32_t* pool, uint32_t off, T v, uint32_t imm = 0) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(pool) + (size_t)off + imm) = v;
+}
+// BE_POOL_MODE (A/B): where a step kernel loads the pool entries of its finished envs.
+//   1: right after done is known, before the physics stores, waited for inside that (divergent)
+//      branch -- only the waves with a finished env wait;
+//   5: inside the reset section (the uniform `if (m)` of the waves with a finished env), after the
+//      stores: the rest of the kernel is the pre-pool code.
+// (Measured and dropped: the loads unwaited in the branch -- the waitcnt pass then drains every
+// outstanding store at the merge before the reset loop, in every wave; branch-free buffer loads with
+// an out-of-range offset for the lanes without a finished env; the loads after the stores outside the
+// reset section.  profiles/r06_pool_ab.txt)
+#ifndef BE_POOL_MODE
+#define BE_POOL_MODE 1
+#endif
+__device__ __forceinline__ uint32_t u4w(const uint4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+__device__ __forceinline__ double u2d(uint32_t lo, uint32_t hi) {
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+constexpr int64_t POOL_MAX_ENVS = 1ll << 22;
 
 // Diagnostics hooks (DBG skip bits, DIAG / PH phase stamps): no-ops in the release build; a
 // -DBE_DIAG_STAMPS / -DBE_DIAG_SKIP build (tools/build_diag.sh, tools/build_ab_lib.sh) defines them.
@@ -888,11 +945,16 @@ __device__ __forceinline__ double reset_dists(int32_t ag, int32_t go, int32_t a0
 // channel of the address in issue order, so the later instruction's bytes win whichever lanes
 // issued the two: the same guarantee a lane relies on for its own two stores to one address
 // (the stores are sc1, none is an atomic).  The rule is per-wave program order, not per lane.
+// Rejection limits (ballenv_env.py:121-126, :145): with rej_own == nullptr the wave ORs
+// BE_STATUS_REJECTION_LIMIT into the status word once per pass; otherwise each owner lane gets its
+// env's flag in *rej_own and the status word is left alone (pool_fill_kernel stores it with the entry,
+// and the step kernel that consumes the entry raises the status bit then).
 template <int WT, int NSC, int NDC, int PMAX, class OSink, class ESink, int LPE = 1>
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
                             uint32_t (&xrows)[Geo<WT>::K], uint32_t* wl, OSink&& osink, ESink&& esink,
-                            const uint64_t* span = nullptr) {   // span: the wave's row-span table (step2_kernel)
+                            const uint64_t* span = nullptr,   // span: the wave's row-span table (step2_kernel)
+                            uint32_t* rej_own = nullptr) {
   // G + 1 lanes per env: lane k < G draws obstacle k, lane G the goal / agent block; every lane
   // runs ONE Philox chain, and the goal lane's four values reach the slot's lanes by readlane
   constexpr int K = Geo<WT>::K, G = NSC + NDC, GL = G + 1, P = (64 / GL < PMAX) ? 64 / GL : PMAX;
@@ -922,6 +984,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
     }
     asm volatile("" : "+v"(il), "+v"(u), "+v"(ep));   // keep the Philox inputs in VGPRs
     const bool act = slot < n;
+    bool rej = false;   // this lane's rejection loop hit its bound
     if (lane < P * K) wrows[lane] = 0u;
     // intra-wave LDS hand-offs: a wave's LDS operations execute in issue order, so only the
     // compiler must keep them in program order (a memory fence would also drain the stores)
@@ -939,7 +1002,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
       rax = map_range(bo.z, 0, t.strip_agent_x); ray = map_range(bo.w, 0, t.strip_agent_y);
       ax0 = rax; ay0 = ray;
       for (int r = 0; d2i(rgx - rax, rgy - ray) < p.min_spawn_d2; ++r) {   // dist < 50 <=> d2 < 2500 (integers)
-        if (r >= REJECT_LIMIT - 1) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+        if (r >= REJECT_LIMIT - 1) { rej = true; break; }
         const u4 b = philox(u, ep, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
         rax = map_range(b.x, 0, t.strip_agent_x); ray = map_range(b.y, 0, t.strip_agent_y);
       }
@@ -964,7 +1027,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
           const bool ra = abs(ox - rax) < rx && 2 * abs(oy - ray) < ry2;
           const bool rg = abs(ox - rgx) < rx && 2 * abs(oy - rgy) < ry2;
           if (!ra && !rg) break;
-          if (a >= REJECT_LIMIT) { atomicOr(p.status, BE_STATUS_REJECTION_LIMIT); break; }
+          if (a >= REJECT_LIMIT) { rej = true; break; }
           bo = philox(u, ep, 0u, tag(PURPOSE_RESET, sub0 | (uint32_t)a), p.seed);
           ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
           oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
@@ -993,6 +1056,8 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
         for (int r = 0; r < K; ++r) atomicOr(&wrows[slot * K + r], mk[r]);
       }
     }
+    const unsigned long long rb = __ballot(rej);
+    if (rb && !rej_own && lane == __ffsll((long long)__ballot(1)) - 1) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     DIAG(13);
@@ -1003,6 +1068,7 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
       const int32_t ag = stash[own * 4 + 0], go = stash[own * 4 + 1], a0 = stash[own * 4 + 2];
       ax = px(ag); ay = py(ag); gx = px(go); gy = py(go);
       esink(own, ag, go, a0);
+      if (rej_own) *rej_own = ((rb >> (own * GL)) & ((1ull << GL) - 1ull)) ? 1u : 0u;
       ncnt = 0;
 #pragma unroll
       for (int r = 0; r < K; ++r) xrows[r] = wrows[own * K + r];
@@ -1728,7 +1794,7 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t x) {   // OR with the other
   return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
 }
 
-template <int WT, int NSC, int NDC>
+template <int WT, int NSC, int NDC, bool POOL = false>
 __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   constexpr int CT = S2_CT;
   constexpr int L = 2, EPW = 64 / L, EPB = CT / L, NWAVE = CT / 64;
@@ -1889,6 +1955,21 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   const bool trunc = p.time_limit > 0 && len >= p.time_limit;
   const bool done = env_done || trunc;
   const bool do_reset = valid && done && p.autoreset;
+  // ---- a finished env's next episode from the autoreset pool: its tag and its 112-byte body (both
+  //      lanes, the same addresses) are loaded here and land while the wave stores the physics
+  const bool ptry = POOL && do_reset;   // (POOL: launched only with a pool, KParams::pool set)
+  uint2 q_tv = make_uint2(0u, 0u);
+  uint4 qb[7];
+#if BE_POOL_MODE == 1
+  if constexpr (POOL) if (ptry) {
+    const uint32_t x = ((episode + 1u) & 1u) * (uint32_t)N + (uint32_t)i;
+    q_tv = pool_ld<uint2>(p.pool, x * 8u);
+    const uint32_t bo = pool_body((uint32_t)N, x, 28);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) qb[j] = pool_ld<uint4>(p.pool, bo, 16u * j);
+    __builtin_amdgcn_s_waitcnt(0);   // here, in the branch: no pending pool load past its end
+  }
+#endif
   if (valid) {   // both lanes of the pair store the env's scalars (the same value to the same address:
                  // one full-wave store per array, no per-lane pointer selects or exec masking)
     const uint32_t iu = (uint32_t)i;
@@ -1921,7 +2002,6 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     if (lane == 0) atomicOr(p.status, (int)f);
   }
   if (DBG(DBG_EXIT_PHYSICS)) return;
-  const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && h == 0);
 
   // ---- episode boundary: terminal obs, then the reset of the finished envs
   uint32_t xrows[KR];
@@ -1935,7 +2015,60 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     flatten<WT>(rows, flat);
     if (!h) write_row_global<WT>(p.terminal_obs + (int64_t)i * F, flat, quadrant(ax, ay, gx, gy));
   }
-  if (m) {   // wave-cooperative: this wave runs its own resets
+  // a pool entry for the new episode (e + 1) that was written and is still current: copy it.  Only
+  // the waves with a finished env take this (uniform) branch, so no other wave waits for the loads
+  // above -- every use of a loaded value is inside it
+  bool hit = false;
+#if BE_POOL_MODE == 5
+  const unsigned long long m0 = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && h == 0);
+  if (m0) {   // (uniform) the waves with a finished env
+  if (POOL) {
+    if (ptry) {
+      const uint32_t x = ((episode + 1u) & 1u) * (uint32_t)N + (uint32_t)i;
+      q_tv = pool_ld<uint2>(p.pool, x * 8u);
+      const uint32_t bo = pool_body((uint32_t)N, x, 28);
+#pragma unroll
+      for (int j = 0; j < 7; ++j) qb[j] = pool_ld<uint4>(p.pool, bo, 16u * j);
+    }
+#else
+  if (__ballot(ptry)) {
+#endif
+    hit = ptry && q_tv.x == episode + 1u && (q_tv.y & POOL_VALID) != 0u;
+    if (hit) {   // both lanes store the env's scalars (as the physics did) and their own obstacle slots
+      auto qw = [&](int k) -> uint32_t { return u4w(qb[k >> 2], k & 3); };   // body word k (compile-time k)
+      const uint32_t iu = (uint32_t)i;
+      const int32_t ag = (int32_t)qw(PB_AGENT), go = (int32_t)qw(PB_GOAL);
+      st_ws(p.ep_return, iu, 0.0);
+      st_ws(p.ep_len, iu, 0);
+      st_ws(p.agent, iu, ag);
+      st_ws(p.prev_dist, iu, u2d(qw(PB_PREV), qw(PB_PREV + 1)));
+      st_ws(p.goal, iu, go);
+      st_ws(p.total_dist, iu, u2d(qw(PB_TOTAL), qw(PB_TOTAL + 1)));
+      st_ws(p.episode, iu, episode + 1u);
+#pragma unroll
+      for (int j = 0; j < SD; ++j) {
+        const int k = L * j + h;
+        const uint32_t o = h ? qw(PB_OBS + NSC + min(L * j + 1, NDC - 1)) : qw(PB_OBS + NSC + L * j);
+        if (k < NDC) {
+          st_ws(p.dyn_obs, (uint32_t)k * (uint32_t)N + iu, (int32_t)o);
+          st_ws(p.dyn_goal, (uint32_t)k * (uint32_t)N + iu, (uint8_t)k);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < SS; ++j) {
+        const int k = L * j + h;
+        const uint32_t o = h ? qw(PB_OBS + min(L * j + 1, NSC - 1)) : qw(PB_OBS + L * j);
+        if (k < NSC) st_ws(p.static_obs, (uint32_t)k * (uint32_t)N + iu, (int32_t)o);
+      }
+      ax = px(ag); ay = py(ag); gx = px(go); gy = py(go);
+#pragma unroll
+      for (int k = 0; k < KR; ++k) xrows[k] = (qw(PB_ROWS + k / 3) >> (10 * (k % 3))) & 0x3FFu;   // three rows per word
+      nl.cnt = 0;
+    }
+    if (__ballot(hit && (q_tv.y & POOL_REJ)) && lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+  }
+  const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && !hit && h == 0);
+  if (m) {   // stale entries (or no pool): wave-cooperative, this wave runs its own resets
     auto osink = [&](int, int k, int il, int32_t o) {   // (32-bit element offsets: pick_kernel keeps NS*N < 2^30)
       if (k < NSC) {
         st_ws(p.static_obs, (uint32_t)k * (uint32_t)N + (uint32_t)il, o);
@@ -1965,6 +2098,9 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
       wave_resets<WT, NSC, NDC, 64, decltype(osink)&, decltype(esink)&, L>(p, t, m, i, gid, episode, ax, ay, gx, gy,
                                                                          nl.cnt, xrows, &s_rows[w][0], osink, esink, span);
   }
+#if BE_POOL_MODE == 5
+  }
+#endif
   DIAG(3);
   if (DBG(DBG_NO_OBS)) return;
   if (DBG(DBG_NO_RASTER)) nl.cnt = 0;
@@ -2058,7 +2194,7 @@ __device__ __forceinline__ uint32_t lane_group_or(uint32_t x) {   // OR over the
   return x;
 }
 
-template <int WT, int NSC, int NDC, int L>
+template <int WT, int NSC, int NDC, int L, bool POOL = false>
 __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   constexpr int CT = 32 * L, EPW = 64 / L, NWAVE = CT / 64;
   constexpr int SS = (NSC + L - 1) / L, SD = (NDC + L - 1) / L;   // obstacle slots per lane
@@ -2210,6 +2346,28 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const bool trunc = p.time_limit > 0 && len >= p.time_limit;
   const bool done = env_done || trunc;
   const bool do_reset = valid && done && p.autoreset;
+  // ---- a finished env's next episode from the autoreset pool, loads issued now (as step2_kernel):
+  //      lane h loads the tag, the body's rows / agent / goal / distances and its own obstacle slots
+  const bool ptry = POOL && do_reset;   // (POOL: launched only with a pool, KParams::pool set)
+  uint2 q_tv = make_uint2(0u, 0u);
+  uint4 q0, q1;
+  uint2 q2;
+  uint32_t q_dp[SD], q_so[SS];
+#if BE_POOL_MODE == 1
+  if constexpr (POOL) if (ptry) {
+    const uint32_t x = ((episode + 1u) & 1u) * (uint32_t)N + (uint32_t)i;
+    q_tv = pool_ld<uint2>(p.pool, x * 8u);
+    const uint32_t bo = pool_body((uint32_t)N, x, 28);
+    q0 = pool_ld<uint4>(p.pool, bo, 0u);     // rows, -, -, agent
+    q1 = pool_ld<uint4>(p.pool, bo, 16u);    // goal, -, prev
+    q2 = pool_ld<uint2>(p.pool, bo, 32u);    // total
+#pragma unroll
+    for (int j = 0; j < SD; ++j) q_dp[j] = pool_ld<uint32_t>(p.pool, bo + 4u * (uint32_t)min(L * j + h, NDC - 1), 4u * (PB_OBS + NSC));
+#pragma unroll
+    for (int j = 0; j < SS; ++j) q_so[j] = pool_ld<uint32_t>(p.pool, bo + 4u * (uint32_t)min(L * j + h, NSC - 1), 4u * PB_OBS);
+    __builtin_amdgcn_s_waitcnt(0);   // here, in the branch: no pending pool load past its end
+  }
+#endif
   if (valid) {   // the per-env scalars: one full-wave store per array
     const uint32_t iu = (uint32_t)i;   // every lane of the group: the same value to the same address
     st_ws(p.reward, iu, reward);
@@ -2247,14 +2405,61 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   }
   PH(4);
   if (DBG(DBG_EXIT_PHYSICS)) return;
-  const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && h == 0);
 
   // ---- episode boundary: terminal obs, then the wave's resets
   if (do_reset && p.terminal_obs && h == 0) {
     const uint32_t fl[Geo<WT>::NW] = {(rows & ((1u << WT) - 1u)) | (rows << WT), 0u};
     write_row_global<WT>(p.terminal_obs + (int64_t)i * F, fl, quadrant(ax, ay, gx, gy));
   }
-  if (m) {
+  // a pool entry for episode e + 1 that was written and is still current: copy it (a uniform branch:
+  // no wave without a finished env waits for the pool loads; every use of a loaded value is inside)
+  bool hit = false;
+  if (__ballot(ptry)) {
+#if BE_POOL_MODE == 5
+    if (ptry) {
+      const uint32_t x = ((episode + 1u) & 1u) * (uint32_t)N + (uint32_t)i;
+      q_tv = pool_ld<uint2>(p.pool, x * 8u);
+      const uint32_t bo = pool_body((uint32_t)N, x, 28);
+      q0 = pool_ld<uint4>(p.pool, bo, 0u);
+      q1 = pool_ld<uint4>(p.pool, bo, 16u);
+      q2 = pool_ld<uint2>(p.pool, bo, 32u);
+#pragma unroll
+      for (int j = 0; j < SD; ++j) q_dp[j] = pool_ld<uint32_t>(p.pool, bo + 4u * (uint32_t)min(L * j + h, NDC - 1), 4u * (PB_OBS + NSC));
+#pragma unroll
+      for (int j = 0; j < SS; ++j) q_so[j] = pool_ld<uint32_t>(p.pool, bo + 4u * (uint32_t)min(L * j + h, NSC - 1), 4u * PB_OBS);
+    }
+#endif
+    hit = ptry && q_tv.x == episode + 1u && (q_tv.y & POOL_VALID) != 0u;
+    if (hit) {   // every lane of the group stores the scalars (as the physics did) and its own slots
+      const uint32_t iu = (uint32_t)i;
+      const int32_t q_ag = (int32_t)q0.w, q_go = (int32_t)q1.x;
+      st_ws(p.agent, iu, q_ag);
+      st_ws(p.goal, iu, q_go);
+      st_ws(p.total_dist, iu, u2d(q2.x, q2.y));
+      st_ws(p.episode, iu, episode + 1u);
+      st_ws(p.ep_return, iu, 0.0);
+      st_ws(p.ep_len, iu, 0);
+      st_ws(p.prev_dist, iu, u2d(q1.z, q1.w));
+#pragma unroll
+      for (int j = 0; j < SD; ++j) {
+        const int k = L * j + h;
+        if (k < NDC) {
+          st_ws(p.dyn_obs, (uint32_t)k * (uint32_t)N + iu, (int32_t)q_dp[j]);
+          st_ws(p.dyn_goal, (uint32_t)k * (uint32_t)N + iu, (uint8_t)k);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < SS; ++j) {
+        const int k = L * j + h;
+        if (k < NSC) st_ws(p.static_obs, (uint32_t)k * (uint32_t)N + iu, (int32_t)q_so[j]);
+      }
+      ax = px(q_ag); ay = py(q_ag); gx = px(q_go); gy = py(q_go);
+      rows = q0.x & 0xFFFFFu;
+    }
+    if (__ballot(hit && (q_tv.y & POOL_REJ)) && lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+  }
+  const unsigned long long m = DBG(DBG_NO_RESET) ? 0ull : __ballot(do_reset && !hit && h == 0);
+  if (m) {   // stale entries (or no pool): the wave's inline resets
     uint32_t xrows[KR];
 #pragma unroll
     for (int k = 0; k < KR; ++k) xrows[k] = 0u;
@@ -2350,6 +2555,83 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
 
   PH(6);
   PH_STORE;
+}
+
+// ------------------------------------------------------------------ the pool's fill
+// pool_fill_kernel<W, NS, ND>: one lane per env; an env at episode e needs the entries of episodes
+// e+1 (slot (e+1) & 1) and e+2 (the other slot).  Each wave ballots its envs with a stale entry per
+// slot and draws them with wave_resets -- the step kernels' own inline reset, so an entry is the
+// reset those kernels would draw, bit for bit -- with sinks into the pool instead of the state.
+// Stream-ordered with the step kernels (be_step queues it every pool_period calls, be_reset and
+// be_load_state after their copies): no step kernel reads an entry while it is written.
+template <int WT, int NSC, int NDC>
+__global__ __launch_bounds__(256) void pool_fill_kernel(KParams p) {
+  constexpr int KR = Geo<WT>::K, NWAVE = 4;
+  static_assert(WT == 10 || WT == 5, "the pool's row packing is laid out for the W = 10 and W = 5 step kernels");
+  __shared__ __align__(16) TablesX t_wave[NWAVE];
+  __shared__ uint32_t s_rows[NWAVE][16 * KR];
+  constexpr int TW = (int)(sizeof(TablesX) / 16);
+  const int N = p.n, tid = (int)threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int i = (int)blockIdx.x * 256 + tid;
+  const bool valid = i < N;
+  const uint32_t ic = (uint32_t)min(i, N - 1), gid = (uint32_t)p.gid0 + (uint32_t)i;
+  constexpr int NBW = pool_body_words(NSC, NDC);
+  uint4 tword[(TW + 63) / 64];
+#pragma unroll
+  for (int j = 0; j < (TW + 63) / 64; ++j)
+    tword[j] = ld_s(reinterpret_cast<const uint4*>(p.tables), (uint32_t)min(lane + j * 64, TW - 1));
+  const uint32_t e = ld_s(p.episode, ic);
+  const uint2 tv0 = pool_ld<uint2>(p.pool, ic * 8u), tv1 = pool_ld<uint2>(p.pool, ((uint32_t)N + ic) * 8u);
+#pragma unroll
+  for (int j = 0; j < (TW + 63) / 64; ++j) reinterpret_cast<uint4*>(&t_wave[w])[min(lane + j * 64, TW - 1)] = tword[j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const Tables& t = t_wave[w].t;
+  const uint64_t* span = span_fits(WT, p.R) ? t_wave[w].span : nullptr;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t target = (((e + 1u) & 1u) == (uint32_t)s) ? e + 1u : e + 2u;   // the episode slot s holds
+    const uint2 tv = s ? tv1 : tv0;
+    const bool need = valid && !(tv.x == target && (tv.y & POOL_VALID));
+    const unsigned long long m = __ballot(need);
+    if (!m) continue;
+    const uint32_t xs = (uint32_t)s * (uint32_t)N;   // this slot's first entry
+    auto osink = [&](int, int k, int il, int32_t o) {   // obstacle k of env il, from the lane that drew it
+      pool_st(p.pool, pool_body((uint32_t)N, xs + (uint32_t)il, NBW), (uint32_t)o, 4u * (uint32_t)(PB_OBS + k));
+    };
+    auto esink = [&](int, int32_t ag, int32_t go, int32_t a0) {   // on the env's own lane
+      double prev;
+      const double td = reset_dists(ag, go, a0, prev);
+      const uint32_t bo = pool_body((uint32_t)N, xs + (uint32_t)i, NBW);
+      pool_st(p.pool, bo, (uint32_t)ag, 4u * PB_AGENT);
+      pool_st(p.pool, bo, (uint32_t)go, 4u * PB_GOAL);
+      pool_st(p.pool, bo, prev, 4u * PB_PREV);
+      pool_st(p.pool, bo, td, 4u * PB_TOTAL);
+    };
+    int ax = 0, ay = 0, gx = 0, gy = 0, ncnt = 0;
+    uint32_t xrows[KR], rej = 0u;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) xrows[k] = 0u;
+    wave_resets<WT, NSC, NDC, 64, decltype(osink)&, decltype(esink)&, 1>(p, t, m, i, gid, target - 1u, ax, ay, gx, gy,
+                                                                         ncnt, xrows, &s_rows[w][0], osink, esink,
+                                                                         span, &rej);
+    if (need) {   // the rows, packed as the consuming kernel ORs its rows, then the tag (written flag)
+      uint32_t q0, q1 = 0u, q2 = 0u;
+      if constexpr (WT == 10) {
+        q0 = xrows[0] | (xrows[1] << 10) | (xrows[2] << 20);
+        q1 = xrows[3] | (xrows[4] << 10) | (xrows[5] << 20);
+        q2 = xrows[6] | (xrows[7] << 10) | (xrows[8] << 20);
+      } else {
+        q0 = xrows[0] | (xrows[1] << 5) | (xrows[2] << 10) | (xrows[3] << 15);
+      }
+      const uint32_t x = xs + (uint32_t)i, bo = pool_body((uint32_t)N, x, NBW);
+      pool_st(p.pool, bo, q0, 4u * PB_ROWS);
+      pool_st(p.pool, bo, q1, 4u * (PB_ROWS + 1));
+      pool_st(p.pool, bo, q2, 4u * (PB_ROWS + 2));
+      pool_st(p.pool, x * 8u, make_uint2(target, POOL_VALID | (rej ? POOL_REJ : 0u)));
+    }
+  }
 }
 
 template <int WT, int NSC, int NDC, int L>
@@ -3110,7 +3392,9 @@ constexpr int FIX_NS = 13, FIX_ND = 5;   // the reference's obstacle counts (bal
 // take the generic kernels, which index in 64 bits.
 constexpr int64_t FIX_MAX_ENVS = 1ll << 29;
 
-Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lanes10 = 1, int lpe5 = 0) {
+// pool: the variant that copies finished envs' resets from the autoreset pool (step2_kernel /
+// stepw_kernel<..., true>; the context passes it only with a pool allocated)
+Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lanes10 = 1, int lpe5 = 0, bool pool = false) {
   int W = c.window;
   const int F = 4 + W * W, nobs = c.num_static + c.num_dynamic;
   Launch L{nullptr, 0, 0, {0}};
@@ -3121,21 +3405,23 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lane
   if (fixed && lanes10 == 2 && W == 10 && span_fits(W, c.radius_obstacle + c.radius_agent) &&
       (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
     // two lanes per env (step2_kernel): 32 envs per wave, 128 per block
-    L.fn = step2_kernel<10, FIX_NS, FIX_ND>;
+    L.fn = pool ? step2_kernel<10, FIX_NS, FIX_ND, true> : step2_kernel<10, FIX_NS, FIX_ND, false>;
     L.epb = S2_CT / 2;
     L.threads = S2_CT;
     constexpr int SLOTS = (FIX_NS + 1) / 2 + (FIX_ND + 1) / 2 + 1;
     L.lds = SLOTS * S2_CT * 4 + L.epb * F;
-    snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d>", FIX_NS, FIX_ND);
+    snprintf(L.name, sizeof L.name, "step2_kernel<10, %d, %d, %s>", FIX_NS, FIX_ND, pool ? "true" : "false");
     return L;
   }
-  if (fixed && W == 5 && (lpe5 == 4 || lpe5 == 8)) {
-    // L lanes per env (stepw_kernel): 32 envs per block
-    L.fn = lpe5 == 8 ? stepw_kernel<5, FIX_NS, FIX_ND, 8> : stepw_kernel<5, FIX_NS, FIX_ND, 4>;
+  if (fixed && W == 5 && (lpe5 == 4 || lpe5 == 8) && (int64_t)c.num_envs * FIX_NS < (1ll << 30)) {
+    // L lanes per env (stepw_kernel): 32 envs per block (its reset sink stores obstacles at 32-bit
+    // byte offsets, as step2_kernel's does: NS*N < 2^30)
+    L.fn = lpe5 == 8 ? (pool ? stepw_kernel<5, FIX_NS, FIX_ND, 8, true> : stepw_kernel<5, FIX_NS, FIX_ND, 8, false>)
+                     : (pool ? stepw_kernel<5, FIX_NS, FIX_ND, 4, true> : stepw_kernel<5, FIX_NS, FIX_ND, 4, false>);
     L.epb = 32;
     L.threads = 32 * lpe5;
     L.lds = 0;
-    snprintf(L.name, sizeof L.name, "stepw_kernel<5, %d, %d, %d>", FIX_NS, FIX_ND, lpe5);
+    snprintf(L.name, sizeof L.name, "stepw_kernel<5, %d, %d, %d, %s>", FIX_NS, FIX_ND, lpe5, pool ? "true" : "false");
     return L;
   }
   if (fixed && W == 10) { L.fn = be_kernel<10, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
@@ -3219,7 +3505,15 @@ struct be_ctx {
   int roll5_lpe;       // W = 5: lanes per env of the fused rollout (1: rollout_kernel; 4 / 8: rolloutw_kernel)
   int max_lds;         // the device's LDS bytes per workgroup
   Launch step_launch[2];   // be_step's kernel without / with the fixed-shape preconditions (fixed per context)
+  Launch step_launch_pool; // the fixed-shape kernel's pool variant (when the context has a pool)
   int64_t blob_hdr[8]; // be_save_state's header (host memory that outlives the async copy)
+  // the autoreset pool (layout at pool_body): allocated when be_step's fixed-shape kernel consumes it
+  uint32_t* pool;      // nullptr: no pool (every reset inline)
+  int64_t pool_bytes;
+  KFn pool_fill;       // pool_fill_kernel<W, 13, 5>
+  int pool_period;     // be_step queues a fill every pool_period step launches (0: only be_reset / be_load_state / be_pool_fill)
+  int pool_calls;      // step launches since the last fill
+  const void* pool_owner;   // the state (its episode array) the pool serves: other states step without it
   mutable struct { KFn fn; int lds; bool ok; } lds_cache[4];   // fits_lds() answers per (kernel, dynamic LDS)
   mutable std::mutex lds_mu;                                    // guards lds_cache (const entries may race)
   char err[512];
@@ -3387,9 +3681,16 @@ const char* be_kernel_name(const be_ctx* ctx, int32_t entry) {
   const bool fixed_ok = !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals;
   Launch L{nullptr, 0, 0, {0}};
   switch (entry) {
-    case BE_ENTRY_STEP_ACTIONS: L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, ctx->step_lanes, ctx->step5_lpe); break;
+    case BE_ENTRY_STEP_ACTIONS:   // (the pool variant when the context has a pool: its state's steps run it)
+      L = pick_kernel(ctx->cfg, MODE_STEP, fixed_ok, ctx->step_lanes, ctx->step5_lpe, ctx->pool != nullptr);
+      break;
     case BE_ENTRY_STEP_SAMPLED: L = pick_kernel(ctx->cfg, MODE_STEP, false); break;
-    case BE_ENTRY_ROLLOUT: L = pick_rollout(ctx->cfg, fixed_ok, ctx->roll5_lpe); if (!fits_lds(ctx, L)) L.fn = nullptr; break;
+    case BE_ENTRY_ROLLOUT: {
+      L = pick_rollout(ctx->cfg, fixed_ok, ctx->roll5_lpe);
+      const DeviceGuard dg(ctx->device);   // fits_lds queries the context's device
+      if (dg.err != hipSuccess || !fits_lds(ctx, L)) L.fn = nullptr;
+      break;
+    }
     case BE_ENTRY_RESET: L = pick_kernel(ctx->cfg, MODE_RESET, false); break;
     case BE_ENTRY_OBSERVE: L = pick_kernel(ctx->cfg, MODE_OBSERVE, false); break;
     default: return nullptr;
@@ -3525,10 +3826,29 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   // be_step's two possible kernels, picked once (pick_kernel formats a name: not per launch)
   ctx->step_launch[0] = pick_kernel(ctx->cfg, MODE_STEP, false, ctx->step_lanes, ctx->step5_lpe);
   ctx->step_launch[1] = pick_kernel(ctx->cfg, MODE_STEP, true, ctx->step_lanes, ctx->step5_lpe);
+  {  // the autoreset pool, for the fixed-shape kernels that consume it (step2_kernel, stepw_kernel)
+    const KFn f = ctx->step_launch[1].fn;
+    const bool consumes = ctx->unit_moves && ctx->distinct_goals && !ctx->generic_only && cfg->autoreset &&
+                          (f == step2_kernel<10, FIX_NS, FIX_ND, false> || f == stepw_kernel<5, FIX_NS, FIX_ND, 8, false> ||
+                           f == stepw_kernel<5, FIX_NS, FIX_ND, 4, false>);
+    bool want = consumes && (int64_t)cfg->num_envs <= POOL_MAX_ENVS;
+    if (const char* v = getenv("BALLENV_POOL")) want = want && strcmp(v, "0") != 0;   // A/B: "0" = no pool
+    ctx->pool_period = 128;
+    if (const char* v = getenv("BALLENV_POOL_PERIOD")) ctx->pool_period = std::max(0, atoi(v));
+    if (want && e == hipSuccess) {
+      ctx->pool_bytes = pool_bytes_per_env(FIX_NS, FIX_ND) * cfg->num_envs;
+      ctx->pool_fill = cfg->window == 10 ? pool_fill_kernel<10, FIX_NS, FIX_ND> : pool_fill_kernel<5, FIX_NS, FIX_ND>;
+      e = hipMalloc(&ctx->pool, (size_t)ctx->pool_bytes);
+      if (e == hipSuccess) e = hipMemset(ctx->pool, 0, (size_t)ctx->pool_bytes);   // every entry unwritten
+      if (e == hipSuccess) e = hipDeviceSynchronize();
+      ctx->step_launch_pool = pick_kernel(ctx->cfg, MODE_STEP, true, ctx->step_lanes, ctx->step5_lpe, true);
+    }
+  }
   if (e != hipSuccess) {
     int rc = fail(nullptr, BE_E_HIP, "HIP error in be_create: %s", hipGetErrorString(e));
     if (ctx->status) (void)hipFree(ctx->status);
     if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+    if (ctx->pool) (void)hipFree(ctx->pool);
     delete ctx;
     return rc;
   }
@@ -3541,6 +3861,7 @@ int be_destroy(be_ctx* ctx) {
   const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
   if (ctx->status) (void)hipFree(ctx->status);
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+  if (ctx->pool) (void)hipFree(ctx->pool);
   delete ctx;
   return BE_OK;
 }
@@ -3571,6 +3892,15 @@ static KParams make_params(be_ctx* ctx, const be_state* st, const be_out* out) {
   return a;
 }
 
+// pool_fill_kernel over every env of the state (the caller holds the DeviceGuard)
+static void launch_pool_fill(be_ctx* ctx, const KParams& a, void* stream) {
+  KParams f = a;
+  f.pool = ctx->pool;
+  const int N = ctx->cfg.num_envs;
+  hipLaunchKernelGGL(ctx->pool_fill, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, f);
+  ctx->pool_calls = 0;
+}
+
 // steps > 1 (be_step_n): `steps` launches of the same kernel, actions advancing by N per step.
 static int launch(be_ctx* ctx, int mode, KParams& a, void* stream, int32_t steps = 1) {
   const bool fixed_ok = mode == MODE_STEP && a.tape == nullptr && a.actions != nullptr && !ctx->generic_only &&
@@ -3579,13 +3909,20 @@ static int launch(be_ctx* ctx, int mode, KParams& a, void* stream, int32_t steps
     return fail(ctx, BE_E_INVALID, "%s", "obs / obs_f32 must be 16-byte aligned");
   const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
   HIP_TRY(ctx, dg.err);
-  const Launch L = mode == MODE_STEP ? ctx->step_launch[fixed_ok ? 1 : 0]
+  // the pool serves one state (its owner: the state last reset / loaded, else the first one stepped);
+  // a step of any other state draws its resets inline, so a context's entries are only ever written
+  // and read by the launches of one state, which the caller orders on its stream anyway
+  if (ctx->pool && mode == MODE_STEP && fixed_ok && !ctx->pool_owner) ctx->pool_owner = a.episode;
+  const bool use_pool = ctx->pool && mode == MODE_STEP && fixed_ok && a.episode == ctx->pool_owner;
+  a.pool = use_pool ? ctx->pool : nullptr;
+  const Launch L = mode == MODE_STEP ? (use_pool ? ctx->step_launch_pool : ctx->step_launch[fixed_ok ? 1 : 0])
                                      : pick_kernel(ctx->cfg, mode, fixed_ok, ctx->step_lanes, ctx->step5_lpe);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)L.threads);
   for (int32_t s = 0; s < steps; ++s) {
     hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
     a.actions += N;
+    if (use_pool && ctx->pool_period > 0 && ++ctx->pool_calls >= ctx->pool_period) launch_pool_fill(ctx, a, stream);
   }
   HIP_TRY(ctx, hipGetLastError());
   return BE_OK;
@@ -3601,7 +3938,15 @@ int be_reset(be_ctx* ctx, const be_state* st, const uint8_t* mask, const int16_t
   a.reward = nullptr; a.done = nullptr; a.truncated = nullptr; a.terminal_obs = nullptr;
   a.final_return = nullptr; a.final_len = nullptr; a.stats = nullptr;
   a.mask = mask; a.reset_tape = reset_tape; a.reset_tape_len = reset_tape ? tape_len : 0;
-  return launch(ctx, MODE_RESET, a, stream);
+  if (int rc = launch(ctx, MODE_RESET, a, stream)) return rc;
+  if (ctx->pool) {   // this state's next two episodes per env, ahead of its first step
+    ctx->pool_owner = st->episode;
+    const DeviceGuard dg(ctx->device);
+    HIP_TRY(ctx, dg.err);
+    launch_pool_fill(ctx, a, stream);
+    HIP_TRY(ctx, hipGetLastError());
+  }
+  return BE_OK;
 }
 
 int be_step(be_ctx* ctx, const be_state* st, const uint8_t* actions, const int16_t* action_deltas,
@@ -3640,7 +3985,13 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
     return fail(ctx, BE_E_INVALID, "%s", "be_rollout needs a 16-byte aligned obs and num_envs * (4+W*W) % 16 == 0");
   if (steps == 0) return BE_OK;
   const Launch L = pick_rollout(ctx->cfg, !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals, ctx->roll5_lpe);
-  if (fits_lds(ctx, L)) {
+  bool fused = false;
+  {   // every HIP query (fits_lds' function attributes) on the context's device
+    const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
+    HIP_TRY(ctx, dg.err);
+    fused = fits_lds(ctx, L);
+  }
+  if (fused) {
     KParams a = make_params(ctx, st, out);
     a.actions = actions; a.steps = steps;
     const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
@@ -3670,14 +4021,14 @@ int be_rollout(be_ctx* ctx, const be_state* st, const uint8_t* actions, int32_t 
 int be_internal_policy_rollout(be_ctx* ctx, const be_state* st, const be_pol_rollout_args* r, void* stream) {
   const Launch L = pick_policy_rollout(ctx->cfg, !ctx->generic_only && ctx->unit_moves && ctx->distinct_goals, r->HT,
                                        r->KS, r->NO);
+  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return; every
+  HIP_TRY(ctx, dg.err);                // HIP query below (fits_lds) runs on the context's device
   if (!fits_lds(ctx, L)) return 0;   // the caller loops select_action + be_step instead
   KParams a = make_params(ctx, st, r->out);
   a.steps = r->steps;
   a.pol_bytes = r->img_bytes; a.pol_actions = r->num_actions; a.pol_img = r->img; a.pol_seed = r->seed;
   a.obs_in = r->obs_in; a.obs_last = r->obs_last;
   a.act_out = r->act->action; a.logp_out = r->act->log_prob; a.value_out = r->act->value;
-  const DeviceGuard dg(ctx->device);   // the caller's current device is restored on return
-  HIP_TRY(ctx, dg.err);
   const int N = ctx->cfg.num_envs;
   const dim3 grid((unsigned)((N + L.epb - 1) / L.epb)), block((unsigned)BLOCK_THREADS);
   hipLaunchKernelGGL(L.fn, grid, block, (size_t)L.lds, (hipStream_t)stream, a);
@@ -3774,6 +4125,80 @@ int be_load_state(be_ctx* ctx, const be_state* st, const void* blob, void* strea
   for (int k = 0; k < 10; ++k)
     if (L.bytes[k] > 0)
       HIP_TRY(ctx, hipMemcpyAsync(dst[k], static_cast<const char*>(blob) + L.off[k], (size_t)L.bytes[k], hipMemcpyDefault, s));
+  if (ctx->pool) {   // the loaded episodes' next entries (the pool's entries need no invalidation:
+                     // each is a pure function of (seed, global id, episode) and is checked by its tag)
+    ctx->pool_owner = st->episode;
+    launch_pool_fill(ctx, make_params(ctx, st, nullptr), stream);
+    HIP_TRY(ctx, hipGetLastError());
+  }
+  return BE_OK;
+}
+
+int be_pool_fill(be_ctx* ctx, const be_state* st, void* stream) {
+  if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
+  if (int rc = check_state(ctx, st)) return rc;
+  if (!ctx->pool) return BE_OK;
+  const DeviceGuard dg(ctx->device);
+  HIP_TRY(ctx, dg.err);
+  ctx->pool_owner = st->episode;
+  launch_pool_fill(ctx, make_params(ctx, st, nullptr), stream);
+  HIP_TRY(ctx, hipGetLastError());
+  return BE_OK;
+}
+
+int be_pool_invalidate(be_ctx* ctx, void* stream) {
+  if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
+  if (!ctx->pool) return BE_OK;
+  const DeviceGuard dg(ctx->device);
+  HIP_TRY(ctx, dg.err);
+  HIP_TRY(ctx, hipMemsetAsync(ctx->pool, 0, (size_t)ctx->pool_bytes, (hipStream_t)stream));
+  return BE_OK;
+}
+
+int be_pool_set_period(be_ctx* ctx, int32_t period) {
+  if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
+  if (period < 0) return fail(ctx, BE_E_INVALID, "%s", "pool period must be >= 0");
+  ctx->pool_period = period;
+  ctx->pool_calls = 0;
+  return BE_OK;
+}
+
+int64_t be_pool_bytes(const be_ctx* ctx) { return ctx && ctx->pool ? ctx->pool_bytes : 0; }
+
+int be_pool_entry(be_ctx* ctx, int32_t env, int32_t slot, uint32_t* words, double* f64, int32_t write) {
+  if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");
+  if (!ctx->pool) return fail(ctx, BE_E_INVALID, "%s", "this context has no autoreset pool");
+  if (env < 0 || env >= ctx->cfg.num_envs || slot < 0 || slot > 1 || !words || !f64)
+    return fail(ctx, BE_E_INVALID, "%s", "bad arguments to be_pool_entry");
+  const DeviceGuard dg(ctx->device);
+  HIP_TRY(ctx, dg.err);
+  HIP_TRY(ctx, hipDeviceSynchronize());
+  // the header's word order (TAG, AGENT, GOAL, ROWS0 | flags << 30, ROWS1, ROWS2, obstacles) from / to
+  // the tags array and the entry body
+  const int64_t n = ctx->cfg.num_envs, x = (int64_t)slot * n + env;
+  constexpr int NBW = pool_body_words(FIX_NS, FIX_ND), NO = FIX_NS + FIX_ND;
+  char* tv = reinterpret_cast<char*>(ctx->pool) + x * 8;
+  char* body = reinterpret_cast<char*>(ctx->pool) + 16 * n + x * 4 * NBW;
+  uint32_t t[2], b[NBW];
+  HIP_TRY(ctx, hipMemcpy(t, tv, sizeof t, hipMemcpyDeviceToHost));
+  HIP_TRY(ctx, hipMemcpy(b, body, sizeof b, hipMemcpyDeviceToHost));
+  if (!write) {
+    words[0] = t[0]; words[1] = b[PB_AGENT]; words[2] = b[PB_GOAL];
+    words[3] = (b[PB_ROWS] & 0x3FFFFFFFu) | ((t[1] & 3u) << 30);
+    words[4] = b[PB_ROWS + 1]; words[5] = b[PB_ROWS + 2];
+    for (int k = 0; k < NO; ++k) words[6 + k] = b[PB_OBS + k];
+    memcpy(&f64[0], &b[PB_PREV], 8);
+    memcpy(&f64[1], &b[PB_TOTAL], 8);
+    return BE_OK;
+  }
+  t[0] = words[0]; t[1] = (words[3] >> 30) & 3u;
+  b[PB_AGENT] = words[1]; b[PB_GOAL] = words[2];
+  b[PB_ROWS] = words[3] & 0x3FFFFFFFu; b[PB_ROWS + 1] = words[4]; b[PB_ROWS + 2] = words[5];
+  for (int k = 0; k < NO; ++k) b[PB_OBS + k] = words[6 + k];
+  memcpy(&b[PB_PREV], &f64[0], 8);
+  memcpy(&b[PB_TOTAL], &f64[1], 8);
+  HIP_TRY(ctx, hipMemcpy(tv, t, sizeof t, hipMemcpyHostToDevice));
+  HIP_TRY(ctx, hipMemcpy(body, b, sizeof b, hipMemcpyHostToDevice));
   return BE_OK;
 }
 

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define BE_ABI_VERSION 6
+#define BE_ABI_VERSION 7
 
 #define BE_MAX_STATIC   64
 #define BE_MAX_DYNAMIC  32
@@ -239,6 +239,32 @@ int be_status(be_ctx* ctx, int32_t* status_out, void* stream);
 int64_t be_state_blob_bytes(const be_config* cfg);
 int be_save_state(be_ctx* ctx, const be_state* st, void* blob, void* stream);
 int be_load_state(be_ctx* ctx, const be_state* st, const void* blob, void* stream);
+
+/* ---- the autoreset pool (a cache inside the context; no reference counterpart) ----
+ * In Philox mode BallEnv.reset (ballenv_env.py:113-167) of env i into episode e is a pure
+ * function of (seed, global id, e) and the config.  When be_step's kernel is a fixed-shape one
+ * that consumes it (step2_kernel at W=10, stepw_kernel at W=5, the reference's 13 + 5 obstacles),
+ * the context holds, per env, the precomputed resets into episodes e+1 and e+2 (ep = the env's
+ * episode); a finishing env copies its entry instead of drawing the reset on the step's critical
+ * path, and draws it inline as before when the entry is stale.  Results are bit-identical either
+ * way -- the pool changes timing only.  be_reset and be_load_state fill it after their own work,
+ * and be_step queues a fill every `period` step launches (default 128; BALLENV_POOL_PERIOD, and
+ * BALLENV_POOL=0 disables the pool, for A/B runs).  The pool serves one state: the one last
+ * reset or loaded (or the first stepped); steps of any other state draw every reset inline, so
+ * entries are only read and written by launches the caller already orders on one stream.
+ * be_pool_fill: fill now (every env's stale entries) and make st the pool's state.
+ * be_pool_invalidate: mark every entry unwritten (async on the stream): the inline path until the
+ * next fill.  be_pool_set_period: fills per step launches (0: only the explicit ones).
+ * be_pool_bytes: the pool's device bytes (0: this context has no pool). */
+int be_pool_fill(be_ctx* ctx, const be_state* st, void* stream);
+int be_pool_invalidate(be_ctx* ctx, void* stream);
+int be_pool_set_period(be_ctx* ctx, int32_t period);
+int64_t be_pool_bytes(const be_ctx* ctx);
+/* Test hook (synchronous; device-wide sync first): read (write = 0) or overwrite (write = 1) env's
+ * entry in slot (0 / 1: the slot of episode x is x & 1).  words: TAG, AGENT, GOAL, ROWS0..2, then
+ * the NS + ND obstacles' packed xy (6 + 13 + 5 words); f64: PREV, TOTAL.  ROWS0 bit 30 marks a
+ * written entry, bit 31 a rejection-limit hit (layout: csrc/ballenv.hip, "the autoreset pool"). */
+int be_pool_entry(be_ctx* ctx, int32_t env, int32_t slot, uint32_t* words, double* f64, int32_t write);
 
 /* ---- on-GPU select_action for batched rollouts (BASELINE config 5) ----
  * Replaces, for every env at once, the caller's per-step

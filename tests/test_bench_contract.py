@@ -47,7 +47,7 @@ def test_bench_json_line(gpu):
     assert d["vs_baseline"] is None and d["config"]["envs_per_gpu"] == 65536 and d["config"]["window"] == 10
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
-    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9 and rf["kernel"] == "step2_kernel<10, 13, 5>"
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9 and rf["kernel"] == "step2_kernel<10, 13, 5, true>"
     assert rf["traffic"] is None or rf["traffic"] > 0
     for leg in ("policy_rollout", "fused_rollout", "board_profile", "config2", "config4", "large_batch", "from_reset"):
         assert d[leg]["value"] > 0, leg
@@ -170,7 +170,15 @@ def test_bench_multi_rank_gloo(gpu):
     d2 = _bench_line(["--gpus", "2", "--dist-backend", "gloo", "--envs", "4096", *common])
     assert d2["ranks"] == 2 and d2["n_gpus"] == 1
     assert d2["config"]["envs_per_gpu"] == 4096 and d2["config"]["global_envs"] == 8192
-    assert d2["value"] > 0 and d2["roofline"]["kernel"] == "step2_kernel<10, 13, 5>"
+    assert d2["value"] > 0 and d2["roofline"]["kernel"] == "step2_kernel<10, 13, 5, true>"
+    # N > 1 explains itself: every rank's own timing, GPU and stats exchange; the line's ms_per_step is
+    # the slowest rank's
+    rows = d2["per_rank"]
+    assert sorted(r["rank"] for r in rows) == [0, 1] and d2["dist_backend"] == "gloo" and d2["rccl_world_size"] is None
+    for r in rows:
+        assert r["kernel_us_mean"] > 0 and r["ms_per_step"] > 0 and r["stats_all_gather_us"] > 0
+        assert r["device_uuid"] and r["envs"] == 4096 and r["env_offset"] == 4096 * r["rank"]
+    assert max(r["ms_per_step"] for r in rows) == d2["ms_per_step"]
     d1 = _bench_line(["--gpus", "1", "--envs", "8192", *common])
     assert d1["ranks"] == 1 and d1["config"]["global_envs"] == 8192
     e1, e2 = d1["episodes"], d2["episodes"]
@@ -195,6 +203,11 @@ def test_bench_config4_split_gloo(gpu):
     assert c2["global_envs"] == c1["global_envs"] == 262144
     assert c2["envs_per_rank"] == 131072 and c1["envs_per_rank"] == 262144 and c2["ranks"] == 2
     assert c2["steps"] == c1["steps"] == 20 and c2["value"] > 0 and c1["value"] > 0
+    rows = c2["per_rank"]                      # per-rank shard timing (the leg's ms_per_step is the max)
+    assert sorted(r["rank"] for r in rows) == [0, 1] and "per_rank" not in c1
+    assert [r["env_offset"] for r in sorted(rows, key=lambda r: r["rank"])] == [0, 131072]
+    assert all(r["kernel_us_mean"] > 0 and r["stats_all_gather_us"] > 0 and r["device_uuid"] for r in rows)
+    assert max(r["ms_per_step"] for r in rows) == c2["ms_per_step"]
     e1, e2 = c1["episodes"], c2["episodes"]
     assert e1["episodes"] > 0 and e2["episodes"] == e1["episodes"]
     assert e2["min_return"] == e1["min_return"] and e2["max_return"] == e1["max_return"]

@@ -130,6 +130,8 @@ def test_entry_points_keep_the_callers_device(gpu):
     from gym_ballenv_amd.config import EnvConfig
     from gym_ballenv_amd.policy import HipPolicy, Policy
     ndev = torch.cuda.device_count()
+    if ndev < 2:   # env and caller on the same device: DeviceGuard would switch nothing
+        pytest.skip("needs two GPUs: with one, the caller's device is the context's and nothing is restored")
     dev = torch.device("cuda", ndev - 1)
     torch.cuda.set_device(0)
     env = BatchedBallEnv(4096, 10, EnvConfig(), device=dev)

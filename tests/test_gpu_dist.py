@@ -62,13 +62,13 @@ def test_multi_rank_engine_matches_one_rank(gpu, tmp_path, E, T, world):
     env.status()
     st = {k: v.cpu().numpy() for k, v in env.state_dict().items()}
     slots = env.stats_buf.cpu().numpy()
-    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5>" if E <= 98304 else "be_kernel<10, 0, 13, 5>")
+    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5, true>" if E <= 98304 else "be_kernel<10, 0, 13, 5>")
 
     assert done.sum() > E * T // 2000, "episodes must finish and autoreset during the run"
     for i, rk in enumerate(ranks):
         off, n = int(rk["off"]), int(rk["n"])
         assert (off, n) == gb.shard(E, i, world)
-        assert str(rk["kernel"]) == "step2_kernel<10, 13, 5>"
+        assert str(rk["kernel"]) == "step2_kernel<10, 13, 5, true>"
         sl = slice(off, off + n)
         np.testing.assert_array_equal(rk["reward"], rew[:, sl], err_msg=f"rank {i} reward")
         np.testing.assert_array_equal(rk["done"], done[:, sl], err_msg=f"rank {i} done")

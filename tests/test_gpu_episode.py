@@ -32,9 +32,9 @@ def fixed_step_kernel(W, N=0):
     one-lane fixed-shape kernel otherwise."""
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     if W == 10 and N <= 96 * 4 * cus:
-        return "step2_kernel<10, 13, 5>"
+        return "step2_kernel<10, 13, 5, true>"
     if W == 5 and N <= 64 * cus:
-        return "stepw_kernel<5, 13, 5, 8>"
+        return "stepw_kernel<5, 13, 5, 8, true>"
     return f"be_kernel<{W}, 0, 13, 5>"
 
 
@@ -336,13 +336,13 @@ def test_step_kernel_dispatch_by_batch(gpu, monkeypatch):
     monkeypatch.delenv("BALLENV_STEP_LPE", raising=False)
     cus = torch.cuda.get_device_properties(gpu).multi_processor_count
     cut = 96 * 4 * cus
-    for N, name in ((cut, "step2_kernel<10, 13, 5>"), (cut + 64, "be_kernel<10, 0, 13, 5>")):
+    for N, name in ((cut, "step2_kernel<10, 13, 5, true>"), (cut + 64, "be_kernel<10, 0, 13, 5>")):
         e = make_env(EnvConfig(), N, 10, gpu, seed=1)
         assert e.kernel_name("step") == name, (N, cus)
         e.close()
     monkeypatch.setenv("BALLENV_STEP_LPE", "2")
     e = make_env(EnvConfig(), cut + 64, 10, gpu, seed=1)
-    assert e.kernel_name("step") == "step2_kernel<10, 13, 5>"
+    assert e.kernel_name("step") == "step2_kernel<10, 13, 5, true>"
     e.close()
 
 
@@ -362,7 +362,7 @@ def test_step2_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
         monkeypatch.setenv("BALLENV_STEP_LPE", lpe)
         envs.append(make_env(cfg_py, N, W, gpu, seed=31, terminal_obs=True, obs_f32=f32))
     monkeypatch.delenv("BALLENV_STEP_LPE")
-    assert envs[0].kernel_name("step") == "step2_kernel<10, 13, 5>"
+    assert envs[0].kernel_name("step") == "step2_kernel<10, 13, 5, true>"
     assert envs[1].kernel_name("step") == "be_kernel<10, 0, 13, 5>"
     lens = torch.from_numpy(_random_lens(N, np.random.default_rng(N), tl)).to(gpu)
     for e in envs:
@@ -408,7 +408,7 @@ def test_step2_span_table_radius_bound(gpu, r_obs):
     N, a, k, W = 8192, 4096, SLICE, 10
     rng = np.random.default_rng(r_obs)
     env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, k, seed=0x5A, rng=rng)
-    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5>" if r_obs + 5 <= 27 else "be_kernel<10, 0, 13, 5>")
+    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5, true>" if r_obs + 5 <= 27 else "be_kernel<10, 0, 13, 5>")
     acts = env.sample_actions(60, seed=0x5A)
     lit = 0
     for t in range(60):
@@ -467,8 +467,8 @@ def test_stepw_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
         monkeypatch.setenv("BALLENV_STEP5_LPE", lpe)
         envs.append(make_env(cfg_py, N, W, gpu, seed=77, terminal_obs=True, obs_f32=f32))
     monkeypatch.delenv("BALLENV_STEP5_LPE")
-    assert [e.kernel_name("step") for e in envs] == ["be_kernel<5, 0, 13, 5>", "stepw_kernel<5, 13, 5, 8>",
-                                                     "stepw_kernel<5, 13, 5, 4>"]
+    assert [e.kernel_name("step") for e in envs] == ["be_kernel<5, 0, 13, 5>", "stepw_kernel<5, 13, 5, 8, true>",
+                                                     "stepw_kernel<5, 13, 5, 4, true>"]
     lens = torch.from_numpy(_random_lens(N, np.random.default_rng(N + tl), tl)).to(gpu)
     for e in envs:
         e.reset()

@@ -42,7 +42,16 @@ def find(prefix):
     return next((k for k in runs if prefix in k), None)
 
 
-head = find("step2_kernel<10, 13, 5>")
+def fills_in(t0, t1, grid):
+    """the autoreset pool's fill launches (pool_fill_kernel, one lane per env) inside [t0, t1]"""
+    out = []
+    for k in runs:
+        if "pool_fill_kernel" in k:
+            out += [x for x in by_grid.get((k, grid), []) if t0 <= x[0] and x[1] <= t1]
+    return out
+
+
+head = find("step2_kernel<10, 13, 5, true>") or find("step2_kernel<10, 13, 5")
 if head:
     L = runs[head]
     lo = a.warmup + a.untimed
@@ -50,16 +59,21 @@ if head:
     print(f"{head}: {len(L)} launches in the whole command; the headline's timed region (launches "
           f"{lo + 1}..{lo + len(reg)}) averages {avg_us(reg):.3f} us per launch; "
           f"65536 x 390 B / that = {65536 * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
+    fl = fills_in(reg[0][0], reg[-1][1], 65536)
+    if fl:
+        per = (sum(e - s for s, e in reg) + sum(e - s for s, e in fl)) / len(reg) / 1e3
+        print(f"  + {len(fl)} pool_fill_kernel launches in that region, {avg_us(fl):.3f} us each: "
+              f"{per:.3f} us of kernel time per step, the fills included")
 for prefix, n, grid, what in (("be_kernel<10, 0, 13, 5>", 262144, 262144, "config 4 at one rank"),
                               ("be_kernel<10, 0, 13, 5>", 131072, 131072, "config 4's 2-GPU shard"),
-                              ("step2_kernel<10, 13, 5>", 32768, 65536, "config 4's 8-GPU shard")):
+                              ("step2_kernel<10, 13, 5, true>", 32768, 65536, "config 4's 8-GPU shard")):
     k = find(prefix)
     L = by_grid.get((k, grid), [])
     if len(L) >= 1000:
         reg = L[-1000:]
         print(f"{k} ({what}, {n} envs): the last 1000 launches at that size average {avg_us(reg):.3f} us; "
               f"{n} x 390 B / that = {n * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
-for prefix, last, what in (("stepw_kernel<5, 13, 5, 8>", 1000, "config 2, 4096 envs, W=5"),
+for prefix, last, what in (("stepw_kernel<5, 13, 5, 8, true>", 1000, "config 2, 4096 envs, W=5"),
                            ("be_kernel<10, 0, 13, 5>", 200, "2^20 envs, large_batch"),
                            ("board_kernel<6, false, 1>", 1000, "createBoard step, 65536 envs"),
                            ("board_kernel<6, true, 1>", 10, "createBoard fused, 100 steps per launch"),
