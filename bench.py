@@ -228,6 +228,21 @@ def timed_graph_steps(graphs, steps, dev, stream, world):
     return el, ev0.elapsed_time(ev1) / steps
 
 
+def pool_info(env):
+    """The autoreset pool of an env's context (include/ballenv.h): every step launch of the timed
+    region is the step kernel plus, every `period` launches, one pool_fill_kernel launch -- the event
+    time per step (kernel_us_mean) includes the fills; a rocprof trace splits the two
+    (tools/trace_regions.py)."""
+    b = env.pool_bytes()
+    if not b:
+        return None
+    p = env.pool_period()
+    return {"bytes": b, "period": p, "fill_kernel": f"pool_fill_kernel<{env.window}, 13, 5>",
+            "fills_per_step": (1.0 / p) if p else 0.0,
+            "note": "kernel_us_mean (HIP events over the timed region) covers the step launches and the "
+                    "fill launches between them"}
+
+
 def rank_rows(dev, row):
     """Per-rank diagnostics of a timed region at N > 1 (the row of every rank, all_gather_object):
     a scaling run then explains its own curve -- which rank / GPU was slow, by how much, and what
@@ -550,6 +565,7 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
     own_el = LAST_OWN_ELAPSED
     env.status()
     kname = env.kernel_name("step")
+    pool = pool_info(env)
     episodes = rows = None
     if global_envs is not None:
         t_ag = time.perf_counter()
@@ -579,6 +595,8 @@ def graph_steps_leg(gb, dev, rank, world, stream, N, W, T, settle, seed=0xBA11, 
         res["episodes"] = episodes
     if rows is not None:
         res["per_rank"] = rows
+    if pool:
+        res["autoreset_pool"] = pool
     return res, kname
 
 
@@ -1063,6 +1081,7 @@ def main():
     # 2 x FETCH_SIZE (gfx950 reports half of wide reads) + WRITE_SIZE, same kernel / envs / W
     # (committed profile, used only when it was taken on the kernel this run launched, same envs/W)
     kname = env.kernel_name("step")
+    headline_pool = pool_info(env)
     pmc = newest_pmc("pmc_step_kernel.json", f"::{kname}(", N)
     traffic, traffic_src = (pmc["hbm_bytes_per_dispatch"], pmc["source"]) if pmc else (None, None)
 
@@ -1084,7 +1103,7 @@ def main():
         roll_res["config2"] = rollout_leg(args, gb, dev, 0, 1, stream, N=args.config2_envs, W=5, env_offset=0,
                                           pmc_suffix="pmc_rollout_config2.json",
                                           label=f"BASELINE config 2: random-action rollout, {args.config2_envs} envs, W=5")
-        off8, n8 = shard(args.config4_envs, 7, 8)
+        off8, n8 = shard(262144, 7, 8)       # BASELINE config 4's batch, whatever --config4-envs says
         roll_res["shard_32768"] = rollout_leg(args, gb, dev, 0, 1, stream, N=n8, W=10, env_offset=off8,
                                               pmc_suffix=f"pmc_rollout_shard_{n8}.json",
                                               label=f"config 4's 8-GPU shard: random-action rollout, {n8} envs "
@@ -1136,6 +1155,8 @@ def main():
             "blocks_obs": blocks_res,
         }
         moved(line["roofline"], B_eng, N, kern_ms * 1e3, pmc)
+        if headline_pool:
+            line["roofline"]["autoreset_pool"] = headline_pool
         line["episodes_note"] = "episodes finished during the timed steps (all ranks)"
         if per_rank_rows is not None:
             # N > 1: each rank's own timing (the line's ms_per_step is the max of these), its GPU, and

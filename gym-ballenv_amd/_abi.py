@@ -26,7 +26,7 @@ EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_by
            "be_last_error", "be_kernel_name",
            "be_create", "be_destroy", "be_reset", "be_step", "be_step_n", "be_rollout", "be_observe", "be_sample_actions",
            "be_status", "be_state_blob_bytes", "be_save_state", "be_load_state",
-           "be_pool_fill", "be_pool_invalidate", "be_pool_set_period", "be_pool_bytes", "be_pool_entry", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
+           "be_pool_fill", "be_pool_invalidate", "be_pool_set_period", "be_pool_period", "be_pool_bytes", "be_pool_entry", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
            "be_policy_rollout", "be_policy_bytes", "be_observe_blocks",
            "be_board_config_default", "be_board_create", "be_board_destroy", "be_board_last_error",
            "be_board_reset", "be_board_step", "be_board_rollout", "be_board_observe", "be_board_status")
@@ -135,6 +135,7 @@ def lib() -> C.CDLL:
         "be_pool_invalidate": (C.c_int, [vp, vp]),
         "be_pool_set_period": (C.c_int, [vp, i32]),
         "be_pool_bytes": (i64, [vp]),
+        "be_pool_period": (i32, [vp]),
         "be_pool_entry": (C.c_int, [vp, i32, i32, P(C.c_uint32), P(C.c_double), i32]),
         "be_policy_create": (C.c_int, [vp, i32, i32, P(vp)]),
         "be_policy_destroy": (C.c_int, [vp]),

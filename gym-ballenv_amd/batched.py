@@ -322,8 +322,10 @@ class BatchedBallEnv:
     # (include/ballenv.h: precomputed next-episode resets the fixed-shape step kernels copy on done;
     # results are bit-identical with or without it -- these calls change timing only)
     def pool_bytes(self) -> int:
-        """Device bytes of this env's autoreset pool (0: its step kernel draws every reset inline)."""
-        return int(self._lib.be_pool_bytes(self._ctx))
+        """Device bytes of this env's autoreset pool (0: its step kernel draws every reset inline;
+        also 0 for a BALLENV_LIB diagnostics build that predates the pool)."""
+        fn = getattr(self._lib, "be_pool_bytes", None)
+        return int(fn(self._ctx)) if fn is not None else 0
 
     def pool_fill(self) -> None:
         """Draw every env's stale entries now (be_pool_fill), on the current stream."""
@@ -332,6 +334,10 @@ class BatchedBallEnv:
     def pool_invalidate(self) -> None:
         """Mark every entry unwritten: resets are drawn inline until the next fill."""
         _abi.check(self._lib.be_pool_invalidate(self._ctx, self._stream()), self._ctx)
+
+    def pool_period(self) -> int:
+        """Step launches per queued fill (0: fills only at reset / load_state / pool_fill)."""
+        return int(self._lib.be_pool_period(self._ctx))
 
     def pool_set_period(self, period: int) -> None:
         """be_step queues a fill every ``period`` steps (0: only reset / load_state / pool_fill)."""

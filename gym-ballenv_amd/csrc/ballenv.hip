@@ -945,10 +945,10 @@ __device__ __forceinline__ double reset_dists(int32_t ag, int32_t go, int32_t a0
 // channel of the address in issue order, so the later instruction's bytes win whichever lanes
 // issued the two: the same guarantee a lane relies on for its own two stores to one address
 // (the stores are sc1, none is an atomic).  The rule is per-wave program order, not per lane.
-// Rejection limits (ballenv_env.py:121-126, :145): with rej_own == nullptr the wave ORs
-// BE_STATUS_REJECTION_LIMIT into the status word once per pass; otherwise each owner lane gets its
-// env's flag in *rej_own and the status word is left alone (pool_fill_kernel stores it with the entry,
-// and the step kernel that consumes the entry raises the status bit then).
+// Rejection limits (ballenv_env.py:121-126, :145): with rej_own == nullptr the lane that hits the
+// bound ORs BE_STATUS_REJECTION_LIMIT into the status word; otherwise each owner lane gets its env's
+// flag in *rej_own and the status word is left alone (pool_fill_kernel stores it with the entry, and
+// the step kernel that consumes the entry raises the status bit then).
 template <int WT, int NSC, int NDC, int PMAX, class OSink, class ESink, int LPE = 1>
 __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long long m, int i, uint32_t gid,
                             uint32_t episode, int& ax, int& ay, int& gx, int& gy, int& ncnt,
@@ -1002,7 +1002,10 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
       rax = map_range(bo.z, 0, t.strip_agent_x); ray = map_range(bo.w, 0, t.strip_agent_y);
       ax0 = rax; ay0 = ray;
       for (int r = 0; d2i(rgx - rax, rgy - ray) < p.min_spawn_d2; ++r) {   // dist < 50 <=> d2 < 2500 (integers)
-        if (r >= REJECT_LIMIT - 1) { rej = true; break; }
+        if (r >= REJECT_LIMIT - 1) {
+          if (!rej_own) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+          rej = true; break;
+        }
         const u4 b = philox(u, ep, 0u, tag(PURPOSE_RESET, 1 + r), p.seed);
         rax = map_range(b.x, 0, t.strip_agent_x); ray = map_range(b.y, 0, t.strip_agent_y);
       }
@@ -1027,7 +1030,10 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
           const bool ra = abs(ox - rax) < rx && 2 * abs(oy - ray) < ry2;
           const bool rg = abs(ox - rgx) < rx && 2 * abs(oy - rgy) < ry2;
           if (!ra && !rg) break;
-          if (a >= REJECT_LIMIT) { rej = true; break; }
+          if (a >= REJECT_LIMIT) {
+            if (!rej_own) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+            rej = true; break;
+          }
           bo = philox(u, ep, 0u, tag(PURPOSE_RESET, sub0 | (uint32_t)a), p.seed);
           ox = map_range(bo.x, t.strip_obs_x, W - t.strip_obs_x);
           oy = map_range(bo.y, t.strip_obs_y, H - t.strip_obs_y);
@@ -1056,8 +1062,9 @@ __device__ void wave_resets(const KParams& p, const Tables& t, unsigned long lon
         for (int r = 0; r < K; ++r) atomicOr(&wrows[slot * K + r], mk[r]);
       }
     }
-    const unsigned long long rb = __ballot(rej);
-    if (rb && !rej_own && lane == __ffsll((long long)__ballot(1)) - 1) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+    // (the step kernels keep the status atomic at the loop's bound, as in round 5: one ballot and a
+    // conditional atomic per pass instead measured 0.08 us slower per step, profiles/r06_pool_ab.txt)
+    const unsigned long long rb = rej_own ? __ballot(rej) : 0ull;
     asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     DIAG(13);
@@ -1957,11 +1964,18 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
   const bool do_reset = valid && done && p.autoreset;
   // ---- a finished env's next episode from the autoreset pool: its tag and its 112-byte body (both
   //      lanes, the same addresses) are loaded here and land while the wave stores the physics
-  const bool ptry = POOL && do_reset;   // (POOL: launched only with a pool, KParams::pool set)
+  // (POOL instances are launched only with KParams::pool set; testing the pointer as well measured
+  // faster -- the compiler schedules the kernel around the branch differently: 5.65-5.71 against
+  // 5.81-5.85 us at 65 536 envs, 4.58-4.59 against 4.78-4.79 at 32 768, profiles/r06_pool_ab.txt)
+  const bool ptry = POOL && do_reset && p.pool != nullptr;
   uint2 q_tv = make_uint2(0u, 0u);
   uint4 qb[7];
-#if BE_POOL_MODE == 1
-  if constexpr (POOL) if (ptry) {
+#if BE_POOL_MODE == 1 || BE_POOL_MODE == 6
+  if constexpr (POOL)
+#if BE_POOL_MODE == 6   // (A/B) a uniform scalar branch around the divergent one
+  if (__ballot(ptry))
+#endif
+  if (ptry) {
     const uint32_t x = ((episode + 1u) & 1u) * (uint32_t)N + (uint32_t)i;
     q_tv = pool_ld<uint2>(p.pool, x * 8u);
     const uint32_t bo = pool_body((uint32_t)N, x, 28);
@@ -2348,7 +2362,10 @@ __global__ __launch_bounds__(32 * L) void stepw_kernel(KParams p) {
   const bool do_reset = valid && done && p.autoreset;
   // ---- a finished env's next episode from the autoreset pool, loads issued now (as step2_kernel):
   //      lane h loads the tag, the body's rows / agent / goal / distances and its own obstacle slots
-  const bool ptry = POOL && do_reset;   // (POOL: launched only with a pool, KParams::pool set)
+  // (POOL instances are launched only with KParams::pool set; testing the pointer as well measured
+  // faster -- the compiler schedules the kernel around the branch differently: 5.65-5.71 against
+  // 5.81-5.85 us at 65 536 envs, 4.58-4.59 against 4.78-4.79 at 32 768, profiles/r06_pool_ab.txt)
+  const bool ptry = POOL && do_reset && p.pool != nullptr;
   uint2 q_tv = make_uint2(0u, 0u);
   uint4 q0, q1;
   uint2 q2;
@@ -4164,6 +4181,8 @@ int be_pool_set_period(be_ctx* ctx, int32_t period) {
 }
 
 int64_t be_pool_bytes(const be_ctx* ctx) { return ctx && ctx->pool ? ctx->pool_bytes : 0; }
+
+int32_t be_pool_period(const be_ctx* ctx) { return ctx ? ctx->pool_period : 0; }
 
 int be_pool_entry(be_ctx* ctx, int32_t env, int32_t slot, uint32_t* words, double* f64, int32_t write) {
   if (!ctx) return fail(nullptr, BE_E_INVALID, "%s", "ctx is NULL");

@@ -254,11 +254,12 @@ int be_load_state(be_ctx* ctx, const be_state* st, const void* blob, void* strea
  * entries are only read and written by launches the caller already orders on one stream.
  * be_pool_fill: fill now (every env's stale entries) and make st the pool's state.
  * be_pool_invalidate: mark every entry unwritten (async on the stream): the inline path until the
- * next fill.  be_pool_set_period: fills per step launches (0: only the explicit ones).
+ * next fill.  be_pool_set_period / be_pool_period: step launches per fill (0: only the explicit ones).
  * be_pool_bytes: the pool's device bytes (0: this context has no pool). */
 int be_pool_fill(be_ctx* ctx, const be_state* st, void* stream);
 int be_pool_invalidate(be_ctx* ctx, void* stream);
 int be_pool_set_period(be_ctx* ctx, int32_t period);
+int32_t be_pool_period(const be_ctx* ctx);
 int64_t be_pool_bytes(const be_ctx* ctx);
 /* Test hook (synchronous; device-wide sync first): read (write = 0) or overwrite (write = 1) env's
  * entry in slot (0 / 1: the slot of episode x is x & 1).  words: TAG, AGENT, GOAL, ROWS0..2, then

@@ -69,6 +69,17 @@ def test_bench_json_line(gpu):
     assert [r["env_offset"] for r in sh] == [131072, 196608, 229376]
     for r in sh:
         assert r["kernel_us_mean"] > 0 and r["projected_node_env_steps_per_s"] > 0 and 0 < r["moved_frac"] <= 1
+    # the headline's autoreset pool, and the fused mode at config 2 and at config 4's 8-GPU shard
+    ap = rf["autoreset_pool"]
+    assert ap["bytes"] > 0 and ap["period"] > 0 and ap["fill_kernel"] == "pool_fill_kernel<10, 13, 5>"
+    assert d["config2"]["autoreset_pool"]["fill_kernel"] == "pool_fill_kernel<5, 13, 5>"
+    fr = d["fused_rollout"]
+    assert fr["config2"]["kernel"] == "rolloutw_kernel<5, 13, 5, 8>" and fr["config2"]["envs"] == 4096
+    assert fr["shard_32768"]["kernel"] == "rollout_kernel<10, 13, 5, 0, 1, 10>" and fr["shard_32768"]["envs"] == 32768
+    assert fr["shard_32768"]["env_offset"] == 229376 and fr["config2"]["window"] == 5
+    for sub in (fr["config2"], fr["shard_32768"]):
+        assert sub["kernel_us_per_step"] > 0 and sub["value"] > 0 and sub["bytes_per_env_step"] > 0
+        assert 0 < sub["moved_frac"] <= 1 and sub["moved_source"]
     eg = d["eager_step"]
     assert eg["value"] > 0 and eg["host_us_per_step_call"] > 0 and eg["gpu_us_per_iteration"] > 0 and eg["steps"] == 50
     check_bench_sources(d)
@@ -84,15 +95,18 @@ def _walk(x, path=""):
             yield from _walk(v, f"{path}[{i}]")
 
 
-def check_bench_sources(d):
+def check_bench_sources(d, fused_sizes=True):
     """Every roofline-bearing leg reports moved_frac <= 1 (the bytes actually moved: PMC, else the
     engine's be_step_bytes); a frac above 1 (SURVEY's 390-B figure) carries frac_note; and every
-    committed profile a leg cites is the NEWEST round's file of that name for that kernel and size."""
+    committed profile a leg cites is the NEWEST round's file of that name for that kernel and size.
+    fused_sizes: the fused rollout's config-2 / 32 768-env sub-lines are required (round 6 on)."""
     import glob
     import re
     want = ["roofline", "config2.roofline", "config4.roofline", "large_batch.roofline", "from_reset.roofline",
             "cold_action_rows", "fused_rollout", "board_profile.roofline", "board_profile.fused.roofline",
             "policy_rollout.roofline", "blocks_obs.envs_65536.u8.roofline"]
+    if fused_sizes:
+        want += ["fused_rollout.config2", "fused_rollout.shard_32768"]
     seen = {p.lstrip("."): x for p, x in _walk(d)}
     for w in want:
         assert w in seen and "moved_frac" in seen[w], w
@@ -123,7 +137,7 @@ def test_bench_source_check_on_the_committed_line():
     if not lines:
         pytest.skip("no committed bench line with the moved_frac fields yet")
     d = json.load(open(lines[-1]))
-    check_bench_sources(d)
+    check_bench_sources(d, fused_sizes=int(os.path.basename(lines[-1])[1:3]) >= 6)
 
 
 def glob_bench_lines():
