@@ -20,6 +20,7 @@ for r in $(seq 1 ${REPS:-3}); do
 import json; d = json.loads(open('$O/$v.$r.log').read().strip().splitlines()[-1])
 s = '%-8s r$r: step %.3f  config2 %.3f  config4@%d %.3f us' % ('$v', d['roofline']['kernel_us_mean'], d['config2']['kernel_us_mean'], d['config4']['envs_per_rank'], d['config4']['kernel_us_mean'])
 if d.get('fused_rollout'): s += '  fused %.3f' % d['fused_rollout']['kernel_us_per_step']
+if d.get('policy_rollout'): s += '  policy %.3f' % d['policy_rollout']['kernel_us_per_step']
 print(s, flush=True)"
   done
 done
