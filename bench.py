@@ -883,7 +883,15 @@ def board_leg(args, gb, dev, rank, world, stream):
                        "random actionArray moves, autoreset, hipGraph replay",
            "value": T * N * world / el, "unit": "env-steps/s", "ms_per_step": el / T * 1e3,
            "kernel_us_mean": ms * 1e3, "bytes_per_env_step": B, "achieved_GBs": B * N / (ms * 1e-3) / 1e9}
-    res["roofline"] = board_roofline(B, N, ms * 1e3, newest_pmc("pmc_board_step.json", "board_kernel<6, false", N))
+    kname = "board_kernel<6, false, 1, true>" if b.pool_bytes() else "board_kernel<6, false, 1, false>"
+    res["kernel"] = kname
+    res["roofline"] = board_roofline(B, N, ms * 1e3, newest_pmc("pmc_board_step.json", kname, N))
+    if b.pool_bytes():   # ballenv.hip's pool for this profile; the fills are inside the timed graph
+        res["roofline"]["autoreset_pool"] = {
+            "bytes": b.pool_bytes(), "fill_period_steps": int(os.environ.get("BALLENV_POOL_PERIOD", "128")),
+            "what": "every env's next two episodes' Philox resets drawn ahead by board_pool_fill (every 128 steps, "
+                    "inside the replayed graph); the step kernel copies a current entry instead of running the "
+                    "reset waves"}
     del g
     # the same rollout fused: be_board_rollout, 100 steps per launch with the state in registers
     Kc = min(100, T)

@@ -29,7 +29,8 @@ EXPORTS = ("be_abi_version", "be_config_default", "be_config_check", "be_step_by
            "be_pool_fill", "be_pool_invalidate", "be_pool_set_period", "be_pool_period", "be_pool_bytes", "be_pool_entry", "be_policy_create", "be_policy_destroy", "be_policy_load", "be_policy_act",
            "be_policy_rollout", "be_policy_bytes", "be_observe_blocks",
            "be_board_config_default", "be_board_create", "be_board_destroy", "be_board_last_error",
-           "be_board_reset", "be_board_step", "be_board_rollout", "be_board_observe", "be_board_status")
+           "be_board_reset", "be_board_step", "be_board_rollout", "be_board_observe", "be_board_status",
+           "be_board_pool_bytes")
 BOARD_MAX_STATIC, BOARD_MAX_ACTIONS, BOARD_FEATURES = 32, 16, 20
 
 
@@ -153,13 +154,14 @@ def lib() -> C.CDLL:
         "be_board_rollout": (C.c_int, [vp, P(BeBoardState), vp, vp, i32, P(BeBoardOut), vp]),
         "be_board_observe": (C.c_int, [vp, P(BeBoardState), P(BeBoardOut), vp]),
         "be_board_status": (C.c_int, [vp, P(i32), vp]),
+        "be_board_pool_bytes": (i64, [vp]),
     }
     # a BALLENV_LIB diagnostics build from an earlier commit (tools/build_rev_lib.sh, A/B runs) may
     # predate the newest entry points and ABI version; the in-tree library must match exactly
     diag = bool(os.environ.get("BALLENV_LIB"))
     for name, (res, args) in sig.items():
         fn = getattr(L, name, None)
-        if fn is None and diag and name.startswith("be_pool_"):
+        if fn is None and diag and (name.startswith("be_pool_") or name == "be_board_pool_bytes"):
             continue
         if fn is None:
             raise BallEnvError(f"{LIB_PATH} does not export {name}: rebuild it")

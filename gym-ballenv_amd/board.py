@@ -150,6 +150,11 @@ class BatchedBoard:
             raise _abi.BallEnvError("device status: " + "; ".join(bits))
         return 0
 
+    def pool_bytes(self) -> int:
+        """Bytes of the autoreset pool (be_board_pool_bytes; 0: every reset drawn inline)."""
+        f = getattr(self._lib, "be_board_pool_bytes", None)
+        return int(f(self._h)) if f is not None and f.restype is not None else 0
+
     def state_dict(self) -> dict:
         return {k: getattr(self, k).clone() for k in self.STATE_KEYS}
 

@@ -37,6 +37,7 @@
 // that needs more: every rejection loop becomes one ballot over 64 candidate attempts).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <math.h>
 #include <new>
 #include <stdint.h>
@@ -75,7 +76,31 @@ struct BParams {
   int32_t steps;                                                   // mode 3
   int32_t W, H, sox, soy, sgx, sgy, sax, say;
   double r_collide, r_feature_obs, r_agent, goal_thr, min_spawn, thr_agent, thr_goal;
+  uint32_t* pool;   // the autoreset pool (below; nullptr: every reset drawn inline)
 };
+
+// ------------------------------------------------------------------ the autoreset pool (createBoard)
+// ballenv.hip's pool for this profile: a Philox reset of env i into episode x is a pure
+// function of (seed, global id, x) and the config, so board_pool_fill draws every env's resets into
+// episodes e+1 and e+2 ahead of time and the per-step kernel copies the entry of a finishing env
+// (its reset pass -- goal, agent and static rejection chains -- was the step's tail), drawing it
+// inline when the entry is stale.  Two entries per env, slot = episode & 1, entry x = slot * N + env:
+//   tags    uint2 [2N] at byte 0       (episode, flags: BPOOL_VALID written, BPOOL_REJ a rejection
+//                                       loop hit its bound)
+//   bodies  [2N] at byte 16 N, 4 * bpool_words(ns) bytes each: agent x, y, goal x, y, state[2] (the
+//           first attempt's distance), total_distance (f64), then the ns statics' packed xy
+constexpr uint32_t BPOOL_VALID = 1u, BPOOL_REJ = 2u;
+__host__ __device__ constexpr int bpool_words(int ns) { return 12 + ((ns + 3) & ~3); }
+constexpr int64_t BPOOL_MAX_ENVS = 1ll << 22;   // every byte offset below 2^32 (48 statics' words at most)
+__device__ __forceinline__ uint32_t bpool_body(uint32_t n, uint32_t x, int ns) { return 16u * n + x * (4u * (uint32_t)bpool_words(ns)); }
+template <class T>
+__device__ __forceinline__ T bp_ld(const uint32_t* pool, uint32_t off, uint32_t imm = 0) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(pool) + (size_t)off + imm);
+}
+template <class T>
+__device__ __forceinline__ void bp_st(uint32_t* pool, uint32_t off, T v, uint32_t imm = 0) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(pool) + (size_t)off + imm) = v;
+}
 
 __device__ __forceinline__ double dist2(double x1, double y1, double x2, double y2) {
   const double dx = x1 - x2, dy = y1 - y2;
@@ -279,10 +304,13 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 // passes (64 agent attempts, 64 / ns per static), which oracle/board_oracle.c restates.  Needs
 // ns <= LS.  The slot's lanes end up holding its env's new state; the env's own lane (the owner)
 // picks it up with uniform readlanes.
-template <int MAXS, int P>
+// OWN (board_pool_fill): the owner lanes get their env's rejection-limit flag in *rej_own and the
+// status word is left alone (the step kernel that consumes the entry raises it).  A template flag,
+// not a null test: the step kernels' instance is the code without the pool, instruction for instruction.
+template <int MAXS, int P, bool OWN = false>
 __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32_t gid, uint32_t episode_new,
                                   double& ax, double& ay, double& gx, double& gy, double& d0, double& total,
-                                  int32_t (&so)[MAXS]) {
+                                  int32_t (&so)[MAXS], uint32_t* rej_own = nullptr) {
   constexpr int LS = 64 / P;
   constexpr unsigned long long SMASK = LS == 64 ? ~0ull : (1ull << LS) - 1;
   constexpr int AG_END = (BOARD_REJECT_LIMIT / 64 + 1) * 64;   // the 64-lane agent passes give up after this
@@ -311,6 +339,7 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
       u = slot == s2 ? u2 : u; ep = slot == s2 ? e2 : ep;
     }
     const bool act = slot < n;
+    [[maybe_unused]] uint32_t rejs = 0u;   // (OWN, uniform) slots whose loops hit the bound in this pass
     // goal (ballenv_pygame.py:462-463), on every lane of the slot
     const u4 bg = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, 0u), p.seed);
     const double rgx = (double)(p.W - p.sgx) + ranf2(bg.x, bg.y) * (double)p.sgx;
@@ -336,7 +365,8 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
         if (!((open >> s2) & 1u)) continue;
         const unsigned long long hit = (ok >> (s2 * LS)) & SMASK;
         if (hit || last) {
-          if (!hit && lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+          if constexpr (OWN) { if (!hit) rejs |= 1u << s2; }
+          else if (!hit && lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
           const int q = s2 * LS + (hit ? __ffsll((long long)hit) - 1 : LS - 1);
           const double x = readlane_f64(cx, q), y = readlane_f64(cy, q);
           rax = slot == s2 ? x : rax; ray = slot == s2 ? y : ray;
@@ -383,7 +413,8 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
             if (hit) {
               v = __builtin_amdgcn_readlane(cand, __ffsll((long long)hit) - 1);
             } else {   // rejection limit: the static's first attempt of the last 64-lane pass
-              if (lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+              if constexpr (OWN) rejs |= 1u << s2;
+              else if (lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
               const u4 bo = philox(u, ep, 0u, tag(PURPOSE_BOARD_RESET, (2u << 20) | ((uint32_t)k << 12) | (uint32_t)st_g0),
                                    p.seed);
               const int ox = p.sox + (int)__umulhi(bo.x, (uint32_t)(p.W - 2 * p.sox));
@@ -405,6 +436,7 @@ __device__ void wave_board_resets(const BParams& p, unsigned long long m, uint32
       const double sax = readlane_f64(rax, src), say = readlane_f64(ray, src), sd0 = readlane_f64(rd0, src);
       const bool own = lane == ls[s2];
       if (own) { gx = sgx; gy = sgy; ax = sax; ay = say; d0 = sd0; total = dist2(sax, say, sgx, sgy); }   // total_distance
+      if constexpr (OWN) { if (own) *rej_own = (rejs >> s2) & 1u; }
 #pragma unroll
       for (int k = 0; k < MAXS; ++k) {
         const int32_t v = __builtin_amdgcn_readlane(got[k], src);
@@ -519,7 +551,7 @@ __device__ __forceinline__ void copy_feat(const float4* stage, float* dst, int n
   }
 }
 
-template <int MAXS, bool ROLL, int L>
+template <int MAXS, bool ROLL, int L, bool POOL = false>
 __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   constexpr int SPL = (MAXS + L - 1) / L, EPW = 64 / L;
   constexpr bool WT = true;   // write-through in both kernels (profiles/r03_board_wt_ab.txt)
@@ -672,6 +704,29 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
       if (m0) {
         const uint32_t g = (uint32_t)p.gid0 + (uint32_t)i;
         unsigned long long m = m0;
+        if constexpr (POOL) {   // (L == 1) the pool's entry for episode + 1 when it is current
+          static_assert(L == 1 && !ROLL, "the pool instance is the one-lane per-step kernel");
+          const bool ptry = do_reset && p.pool != nullptr;
+          uint2 q_tv = make_uint2(0u, 0u);
+          double2 qa = make_double2(0.0, 0.0), qg = qa, qd = qa;
+          if (ptry) {   // (the statics load straight into so: a finishing lane's are dead, and a stale
+                        // entry's lane gets them again from the inline passes below)
+            const uint32_t x = ((episode + 1u) & 1u) * (uint32_t)p.n + (uint32_t)i;
+            q_tv = bp_ld<uint2>(p.pool, x * 8u);
+            const uint32_t bo = bpool_body((uint32_t)p.n, x, p.ns);
+            qa = bp_ld<double2>(p.pool, bo, 0u);
+            qg = bp_ld<double2>(p.pool, bo, 16u);
+            qd = bp_ld<double2>(p.pool, bo, 32u);
+#pragma unroll
+            for (int k = 0; k < MAXS; ++k)
+              if (k < p.ns) so[k] = bp_ld<int32_t>(p.pool, bo, 48u + 4u * (uint32_t)k);
+            __builtin_amdgcn_s_waitcnt(0);   // here, in the branch: no pending pool load past its end
+          }
+          const bool hit = ptry && q_tv.x == episode + 1u && (q_tv.y & BPOOL_VALID) != 0u;
+          if (hit) { ax = qa.x; ay = qa.y; gx = qg.x; gy = qg.y; dist = qd.x; total = qd.y; }
+          if (__ballot(hit && (q_tv.y & BPOOL_REJ)) && lane == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+          m = __ballot(do_reset && !hit);
+        }
         if constexpr (MAXS <= 12) {   // one Philox chain per reset; the rare rest take the general passes
           if (p.ns >= 1) m = wave_board_resets_fast<MAXS>(p, m, g, episode + 1u, ax, ay, gx, gy, dist, total, so);
         }
@@ -737,6 +792,56 @@ __global__ __launch_bounds__(256) void board_kernel(BParams p) {
   }
 }
 
+// The pool's fill (one lane per env): an env at episode e needs the entries of e+1 (slot (e+1) & 1)
+// and e+2; a wave draws its stale ones with the step kernel's own passes (the single-chain pass,
+// then the general passes for its rest), so an entry is the reset the step would draw, bit for bit.
+// Stream-ordered with the steps (be_board_step queues it every pool period, be_board_reset after its
+// kernel).
+template <int MAXS>
+__global__ __launch_bounds__(256) void board_pool_fill(BParams p) {
+  const int i0 = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  const bool valid = i0 < p.n;
+  const int i = valid ? i0 : p.n - 1;
+  const uint32_t g = (uint32_t)p.gid0 + (uint32_t)i, e = p.episode[i];
+  const uint2 tv0 = bp_ld<uint2>(p.pool, (uint32_t)i * 8u), tv1 = bp_ld<uint2>(p.pool, ((uint32_t)p.n + (uint32_t)i) * 8u);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t target = (((e + 1u) & 1u) == (uint32_t)s) ? e + 1u : e + 2u;   // the episode slot s holds
+    const uint2 tv = s ? tv1 : tv0;
+    const bool need = valid && !(tv.x == target && (tv.y & BPOOL_VALID));
+    unsigned long long m = __ballot(need);
+    if (!m) continue;
+    double ax = 0.0, ay = 0.0, gx = 0.0, gy = 0.0, d0 = 0.0, total = 0.0;
+    int32_t so[MAXS];
+#pragma unroll
+    for (int k = 0; k < MAXS; ++k) so[k] = 0;
+    uint32_t rej = 0u;
+    if constexpr (MAXS <= 12) {
+      if (p.ns >= 1) m = wave_board_resets_fast<MAXS>(p, m, g, target, ax, ay, gx, gy, d0, total, so);
+    }
+    if (m) {
+      const int nf = __popcll(m);
+      if constexpr (MAXS > 16) {
+        wave_board_resets<MAXS, 1, true>(p, m, g, target, ax, ay, gx, gy, d0, total, so, &rej);
+      } else {
+        if (nf == 1) wave_board_resets<MAXS, 1, true>(p, m, g, target, ax, ay, gx, gy, d0, total, so, &rej);
+        else if (nf == 2 || p.ns > 8) wave_board_resets<MAXS, 2, true>(p, m, g, target, ax, ay, gx, gy, d0, total, so, &rej);
+        else wave_board_resets<MAXS, 4, true>(p, m, g, target, ax, ay, gx, gy, d0, total, so, &rej);
+      }
+    }
+    if (need) {   // the body, then the tag (its written flag)
+      const uint32_t x = (uint32_t)s * (uint32_t)p.n + (uint32_t)i, bo = bpool_body((uint32_t)p.n, x, p.ns);
+      bp_st(p.pool, bo, make_double2(ax, ay), 0u);
+      bp_st(p.pool, bo, make_double2(gx, gy), 16u);
+      bp_st(p.pool, bo, make_double2(d0, total), 32u);
+#pragma unroll
+      for (int k = 0; k < MAXS; ++k)
+        if (k < p.ns) bp_st(p.pool, bo, so[k], 48u + 4u * (uint32_t)k);
+      bp_st(p.pool, x * 8u, make_uint2(target, BPOOL_VALID | (rej ? BPOOL_REJ : 0u)));
+    }
+  }
+}
+
 }  // namespace
 
 struct be_board {
@@ -745,6 +850,10 @@ struct be_board {
   bool lpe2;           // BALLENV_BOARD_LPE=2: two lanes per env (A/B)
   int* status;
   BoardTables* d_tables;
+  uint32_t* pool;      // the autoreset pool (Philox autoreset, one lane per env), or nullptr
+  int64_t pool_bytes;
+  int pool_period, pool_calls;
+  const void* pool_owner;   // the state (its episode array) the pool serves
   char err[512];
 };
 
@@ -806,10 +915,23 @@ int be_board_create(const be_board_config* cfg, int32_t device, be_board** out) 
   if (e == hipSuccess) e = hipMemset(b->status, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc(&b->d_tables, sizeof t);
   if (e == hipSuccess) e = hipMemcpy(b->d_tables, &t, sizeof t, hipMemcpyHostToDevice);
+  {  // the autoreset pool: Philox autoreset, one lane per env (BALLENV_POOL=0 disables it, A/B)
+    bool want = cfg->autoreset && !b->lpe2 && (int64_t)cfg->num_envs <= BPOOL_MAX_ENVS;
+    if (const char* v = getenv("BALLENV_POOL")) want = want && strcmp(v, "0") != 0;
+    b->pool_period = 128;
+    if (const char* v = getenv("BALLENV_POOL_PERIOD")) b->pool_period = std::max(0, atoi(v));
+    if (want && e == hipSuccess) {
+      b->pool_bytes = 2ll * cfg->num_envs * (8 + 4ll * bpool_words(cfg->num_static));
+      e = hipMalloc(&b->pool, (size_t)b->pool_bytes);
+      if (e == hipSuccess) e = hipMemset(b->pool, 0, (size_t)b->pool_bytes);   // every entry unwritten
+      if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
+  }
   if (e != hipSuccess) {
     const int rc = bhip(nullptr, e);
     if (b->status) (void)hipFree(b->status);
     if (b->d_tables) (void)hipFree(b->d_tables);
+    if (b->pool) (void)hipFree(b->pool);
     delete b;
     return rc;
   }
@@ -822,9 +944,12 @@ int be_board_destroy(be_board* b) {
   const DeviceGuard dg(b->device);   // the caller's current device is restored on return
   if (b->status) (void)hipFree(b->status);
   if (b->d_tables) (void)hipFree(b->d_tables);
+  if (b->pool) (void)hipFree(b->pool);
   delete b;
   return BE_OK;
 }
+
+int64_t be_board_pool_bytes(const be_board* b) { return b && b->pool ? b->pool_bytes : 0; }
 
 const char* be_board_last_error(const be_board* b) { return b ? b->err : g_board_err; }
 
@@ -867,16 +992,36 @@ static int board_launch(be_board* b, const be_board_state* st, const be_board_ou
   // and 4.96 vs 3.97 us fused at 65 536 envs -- the per-env f64 chains (acos, hypot, the reward
   // divide) run on both lanes and outweigh the halved obstacle terms (profiles/r03_board_lanes_ab.txt)
   const int lpe = (tape || !b->lpe2) ? 1 : 2;
+  // the pool serves one state (the one last reset, else the first one stepped): its steps run the
+  // pool instance, any other state's steps draw every reset inline
+  if (b->pool && mode == 0 && !b->pool_owner) b->pool_owner = st->episode;
+  const bool use_pool = b->pool && mode == 0 && lpe == 1 && st->episode == b->pool_owner;
+  p.pool = use_pool ? b->pool : nullptr;
   void (*fn)(BParams) = nullptr;
-#define BE_BOARD_PICK(R, LL)                                                                   \
-  fn = c.num_static <= 4 ? board_kernel<4, R, LL> : c.num_static <= 6 ? board_kernel<6, R, LL>  \
-     : c.num_static <= 8 ? board_kernel<8, R, LL> : c.num_static <= 12 ? board_kernel<12, R, LL> \
-     : c.num_static <= 16 ? board_kernel<16, R, LL> : board_kernel<32, R, LL>
+#define BE_BOARD_PICK(R, LL, ...)                                                                                       \
+  fn = c.num_static <= 4 ? board_kernel<4, R, LL, ##__VA_ARGS__> : c.num_static <= 6 ? board_kernel<6, R, LL, ##__VA_ARGS__>   \
+     : c.num_static <= 8 ? board_kernel<8, R, LL, ##__VA_ARGS__> : c.num_static <= 12 ? board_kernel<12, R, LL, ##__VA_ARGS__> \
+     : c.num_static <= 16 ? board_kernel<16, R, LL, ##__VA_ARGS__> : board_kernel<32, R, LL, ##__VA_ARGS__>
   if (mode == 3) { if (lpe == 2) BE_BOARD_PICK(true, 2); else BE_BOARD_PICK(true, 1); }
+  else if (use_pool) BE_BOARD_PICK(false, 1, true);
   else { if (lpe == 2) BE_BOARD_PICK(false, 2); else BE_BOARD_PICK(false, 1); }
 #undef BE_BOARD_PICK
   const int epb = 256 / lpe;
   hipLaunchKernelGGL(fn, dim3((unsigned)((c.num_envs + epb - 1) / epb)), dim3(256), 0, (hipStream_t)stream, p);
+  // the pool's fill: after a reset (its state's next two episodes), and every pool period of steps
+  const bool fill = b->pool && (mode == 1 || (use_pool && b->pool_period > 0 && ++b->pool_calls >= b->pool_period));
+  if (fill) {
+    if (mode == 1) b->pool_owner = st->episode;
+    if (st->episode == b->pool_owner) {
+      b->pool_calls = 0;
+      BParams f = p;
+      f.pool = b->pool; f.tape = nullptr; f.tape_len = 0;
+      void (*ff)(BParams) = c.num_static <= 4 ? board_pool_fill<4> : c.num_static <= 6 ? board_pool_fill<6>
+                          : c.num_static <= 8 ? board_pool_fill<8> : c.num_static <= 12 ? board_pool_fill<12>
+                          : c.num_static <= 16 ? board_pool_fill<16> : board_pool_fill<32>;
+      hipLaunchKernelGGL(ff, dim3((unsigned)((c.num_envs + 255) / 256)), dim3(256), 0, (hipStream_t)stream, f);
+    }
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return bhip(b, e);
   return BE_OK;

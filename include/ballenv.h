@@ -390,6 +390,12 @@ int be_board_rollout(be_board* b, const be_board_state* st, const uint8_t* actio
                      int32_t steps, const be_board_out* out, void* stream);
 int be_board_observe(be_board* b, const be_board_state* st, const be_board_out* out, void* stream);
 int be_board_status(be_board* b, int32_t* status_out, void* stream);
+/* The board's autoreset pool (as be_pool_* above): with Philox autoreset and one lane
+ * per env, be_board_reset queues a fill of every env's next two episodes' resets and be_board_step
+ * one every 128 steps (BALLENV_POOL_PERIOD), and the steps of the state last reset copy a current
+ * entry where they would draw the reset inline -- the same bits either way.  BALLENV_POOL=0 at
+ * create disables it.  Bytes held (0: no pool). */
+int64_t be_board_pool_bytes(const be_board* b);
 
 #ifdef __cplusplus
 }

@@ -348,3 +348,59 @@ def test_gpu_board_top_of_id_space(gpu):
     assert n_done > k // 50, n_done
     b.status()
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ns,period,over", [(6, "128", {}), (13, "1", {}), (0, "3", {}), (20, "0", {}),
+                                            (8, "5", {"min_spawn_dist": 65.0}), (6, "2", {"min_spawn_dist": 200.0})])
+def test_gpu_board_pool_equals_inline(gpu, ns, period, over, monkeypatch):
+    """The board's autoreset pool (be_board_pool_bytes > 0) changes no bit: be_board_step with the
+    pool equals the inline draws (BALLENV_POOL=0) -- features, rewards, dones, truncations and state
+    through autoresets, for a fill every step (period 1), a short period, the default, and no periodic
+    fill (period 0: entries go stale after the first two episodes and the steps fall back to inline
+    draws); general-pass envs (min_spawn 65) and an impossible spawn rule (every reset at the
+    rejection limit: the REJ flag raises the status word as the inline draw does).  A masked reset
+    mid-run refills the pool; a state_dict round trip (episode counters rewound) leaves the tags to
+    reject what no longer matches."""
+    N, K = 5000, 60
+    boards = []
+    for pool in ("1", "0"):
+        monkeypatch.setenv("BALLENV_POOL", pool)
+        monkeypatch.setenv("BALLENV_POOL_PERIOD", period)
+        boards.append(make_board(gpu, N, ns, seed=21, autoreset=True, time_limit=15, **over))
+    monkeypatch.delenv("BALLENV_POOL")
+    monkeypatch.delenv("BALLENV_POOL_PERIOD")
+    assert boards[0].pool_bytes() > 0 and boards[1].pool_bytes() == 0
+    for b in boards:
+        b.reset()
+    snap = boards[0].state_dict()
+    g = torch.Generator(device="cpu").manual_seed(ns + 1)
+    mv = torch.randint(0, 4, (K, N), generator=g, dtype=torch.uint8).to(gpu)
+    mask = torch.rand(N, generator=g) < 0.4
+    n_done = 0
+    for t in range(K):
+        if t == 20:
+            for b in boards:
+                b.reset(mask=mask)
+        if t == 40:
+            for b in boards:
+                b.load_state_dict(snap)
+        res = [b.step(mv[t]) for b in boards]
+        for x, y in zip(res[0][:3], res[1][:3]):
+            assert torch.equal(x, y), t
+        assert torch.equal(res[0][3]["truncated"], res[1][3]["truncated"]), t
+        n_done += int(res[0][2].sum())
+        for k in boards[0].STATE_KEYS:
+            assert torch.equal(getattr(boards[0], k), getattr(boards[1], k)), (t, k)
+    assert n_done > N
+    errs = []
+    for b in boards:
+        try:
+            b.status()
+            errs.append(None)
+        except Exception as e:   # the impossible spawn rule: both raise the rejection limit
+            errs.append(str(e))
+    assert errs[0] == errs[1]
+    assert (errs[0] is not None) == (over.get("min_spawn_dist", 0) > 150), errs
+    for b in boards:
+        b.close()

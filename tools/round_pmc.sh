@@ -16,5 +16,5 @@ python3 tools/pmc_report.py $O/c2 "be_kernel<10, 0, 13, 5>" 1048576 --out $O/${R
 PASSES="FETCH_SIZE WRITE_SIZE sq1 sq2" timeout -k 10 900 bash tools/pmc_passes.sh ${R}_pmc/board --no-cpu-baseline --steps 10 --warmup 2 \
     --settle 10 --policy-steps 0 --torch-policy-steps 0 --board-steps 200 --board-cpu-seconds 0 --rollout-steps 0 --cold-steps 0 \
     --config2-steps 0 --config4-steps 0 --large-steps 0 --from-reset-steps 0 --blocks-launches 0 --shard-steps 0 --eager-steps 0 || exit 1
-python3 tools/pmc_report.py $O/board "board_kernel<6, false" 65536 --out $O/${R}_pmc_board_step.json | tail -2
+python3 tools/pmc_report.py $O/board "board_kernel<6, false, 1, true>" 65536 --out $O/${R}_pmc_board_step.json | tail -2
 python3 tools/pmc_report.py $O/board "board_kernel<6, true" 6553600 --out $O/${R}_pmc_board_rollout.json | tail -2

@@ -42,11 +42,11 @@ def find(prefix):
     return next((k for k in runs if prefix in k), None)
 
 
-def fills_in(t0, t1, grid):
-    """the autoreset pool's fill launches (pool_fill_kernel, one lane per env) inside [t0, t1]"""
+def fills_in(t0, t1, grid, name="pool_fill_kernel"):
+    """the autoreset pool's fill launches (pool_fill_kernel / board_pool_fill, one lane per env) inside [t0, t1]"""
     out = []
     for k in runs:
-        if "pool_fill_kernel" in k:
+        if name in k:
             out += [x for x in by_grid.get((k, grid), []) if t0 <= x[0] and x[1] <= t1]
     return out
 
@@ -75,11 +75,18 @@ for prefix, n, grid, what in (("be_kernel<10, 0, 13, 5>", 262144, 262144, "confi
               f"{n} x 390 B / that = {n * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
 for prefix, last, what in (("stepw_kernel<5, 13, 5, 8, true>", 1000, "config 2, 4096 envs, W=5"),
                            ("be_kernel<10, 0, 13, 5>", 200, "2^20 envs, large_batch"),
-                           ("board_kernel<6, false, 1>", 1000, "createBoard step, 65536 envs"),
-                           ("board_kernel<6, true, 1>", 10, "createBoard fused, 100 steps per launch"),
+                           ("board_kernel<6, false, 1", 1000, "createBoard step, 65536 envs"),
+                           ("board_kernel<6, true, 1", 10, "createBoard fused, 100 steps per launch"),
                            ("rollout_kernel<10, 13, 5, 13, 2, 10>", 10, "config 5 fused, 100 steps per launch"),
                            ("blocks_kernel", 200, "prep_state2 blocks (last leg size)")):
     k = find(prefix)
     if k:
         L = runs[k]
         print(f"{k} ({what}): {len(L)} launches; the last {min(last, len(L))} average {avg_us(L[-last:]):.3f} us")
+        if prefix.startswith("board_kernel<6, false"):
+            reg = L[-last:]
+            fl = fills_in(reg[0][0], reg[-1][1], 65536, "board_pool_fill")
+            if fl:
+                per = (sum(e - s for s, e in reg) + sum(e - s for s, e in fl)) / len(reg) / 1e3
+                print(f"  + {len(fl)} board_pool_fill launches among them, {avg_us(fl):.3f} us each: "
+                      f"{per:.3f} us of kernel time per step, the fills included")
