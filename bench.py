@@ -804,10 +804,15 @@ def newest_pmc(suffix, kernel_sub, units):
     for path in glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_" + suffix)):
         m = re.match(r"r(\d\d)_", os.path.basename(path))
         found.append((int(m.group(1)), path))
+    # a round-6 `..., false>` instance (no autoreset pool) is instruction for instruction the kernel
+    # of the same name without the flag in earlier rounds, so those profiles stand for it
+    subs = [kernel_sub]
+    if kernel_sub.endswith(", false>") or kernel_sub.endswith(", false>("):
+        subs.append(kernel_sub.replace(", false>", ">"))
     for rnd, path in sorted(found, reverse=True):
         d = json.load(open(path))
         u = d.get("units_per_dispatch", d.get("envs"))
-        if u != units or kernel_sub not in (d.get("kernel") or ""):
+        if u != units or not any(k in (d.get("kernel") or "") for k in subs):
             continue
         d.setdefault("hbm_bytes_per_dispatch", d.get("hbm_bytes_per_launch"))
         d.setdefault("hbm_bytes_per_unit", d["hbm_bytes_per_dispatch"] / units)

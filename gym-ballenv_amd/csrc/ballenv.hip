@@ -1114,9 +1114,12 @@ __device__ __forceinline__ void raster_fixed(const NearList<BLOCK_THREADS>& nl, 
   }
 }
 
-template <int WT, int MODE, int NSC = 0, int NDC = 0>
+// POOL (the fixed-shape step only): a finishing env copies its autoreset-pool entry (§3.10) when it
+// is current; the false instances are the code without the pool
+template <int WT, int MODE, int NSC = 0, int NDC = 0, bool POOL = false>
 __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
   constexpr bool FIXED = NSC > 0 || NDC > 0;
+  static_assert(!POOL || (FIXED && MODE == MODE_STEP && (WT == 10 || WT == 5)), "the pool: fixed-shape steps at W = 10 / 5");
   constexpr int LPE = FIXED ? 1 : lanes_for(WT);
   constexpr int EPB = BLOCK_THREADS / LPE;
   static_assert(!FIXED || (MODE == MODE_STEP && WT > 0 && NSC <= CS && NDC <= CD), "fixed-shape kernels: step only");
@@ -1525,7 +1528,52 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
 #pragma unroll
   for (int k = 0; k < KR; ++k) xrows[k] = 0u;
   if constexpr (FIXED) {
-    const unsigned long long m = __ballot(valid && do_reset);
+    bool hit = false;
+    if constexpr (POOL) {   // the entry for episode + 1 (its tag and 112-byte body), waited for in the branch
+      constexpr int NBW = pool_body_words(NSC, NDC);
+      static_assert(NBW == 28, "seven 16-byte body loads");
+      const bool ptry = valid && do_reset && p.pool != nullptr;
+      uint2 q_tv = make_uint2(0u, 0u);
+      uint4 qb[7];
+      if (ptry) {
+        const uint32_t x = ((episode + 1u) & 1u) * (uint32_t)N + (uint32_t)i;
+        q_tv = pool_ld<uint2>(p.pool, x * 8u);
+        const uint32_t bo = pool_body((uint32_t)N, x, NBW);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) qb[j] = pool_ld<uint4>(p.pool, bo, 16u * j);
+        __builtin_amdgcn_s_waitcnt(0);   // here, in the branch: no pending pool load past its end
+      }
+      if (__ballot(ptry)) {
+        hit = ptry && q_tv.x == episode + 1u && (q_tv.y & POOL_VALID) != 0u;
+        if (hit) {   // the new state as esink / osink below store it, then the rows for the obs
+          auto qw = [&](int k) -> uint32_t { return u4w(qb[k >> 2], k & 3); };   // body word k (compile-time k)
+          const uint32_t iu = (uint32_t)i;
+          const int32_t ag = (int32_t)qw(PB_AGENT), go = (int32_t)qw(PB_GOAL);
+          st_ws(p.agent, iu, ag);
+          st_ws(p.goal, iu, go);
+          st_ws(p.prev_dist, iu, u2d(qw(PB_PREV), qw(PB_PREV + 1)));
+          st_ws(p.total_dist, iu, u2d(qw(PB_TOTAL), qw(PB_TOTAL + 1)));
+          st_ws(p.ep_return, iu, 0.0);
+          st_ws(p.ep_len, iu, 0);
+          st_ws(p.episode, iu, episode + 1u);
+#pragma unroll
+          for (int k = 0; k < NSC; ++k) st_ws(p.static_obs + (size_t)k * N, iu, (int32_t)qw(PB_OBS + k));
+#pragma unroll
+          for (int k = 0; k < NDC; ++k) {
+            st_ws(p.dyn_obs + (size_t)k * N, iu, (int32_t)qw(PB_OBS + NSC + k));
+            st_ws(p.dyn_goal + (size_t)k * N, iu, (uint8_t)k);
+          }
+          ax = px(ag); ay = py(ag); gx = px(go); gy = py(go);
+#pragma unroll
+          for (int k = 0; k < KR; ++k)
+            xrows[k] = WT == 10 ? (qw(PB_ROWS + k / 3) >> (10 * (k % 3))) & 0x3FFu   // three rows per word
+                                : (qw(PB_ROWS) >> (5 * k)) & 0x1Fu;                  // W = 5: four in one
+          nl.cnt = 0;
+        }
+        if (__ballot(hit && (q_tv.y & POOL_REJ)) && (tid & 63) == 0) atomicOr(p.status, BE_STATUS_REJECTION_LIMIT);
+      }
+    }
+    const unsigned long long m = __ballot(valid && do_reset && !hit);
     static_assert(!FIXED || (RCAP >= (BLOCK_THREADS / 64) * 16 && 16 * KR >= (64 / (NSC + NDC + !FIXED)) * (KR + 4)), "wave reset scratch");
     // one finished env (the common case): the lean single-env pass; several: up to 3 per pass
     // a reset env's new state goes straight to HBM
@@ -3441,8 +3489,13 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lane
     snprintf(L.name, sizeof L.name, "stepw_kernel<5, %d, %d, %d, %s>", FIX_NS, FIX_ND, lpe5, pool ? "true" : "false");
     return L;
   }
-  if (fixed && W == 10) { L.fn = be_kernel<10, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
-  else if (fixed && W == 5) { L.fn = be_kernel<5, MODE_STEP, FIX_NS, FIX_ND>; L.epb = BLOCK_THREADS; W = -1; }
+  if (fixed && W == 10) {
+    L.fn = pool ? be_kernel<10, MODE_STEP, FIX_NS, FIX_ND, true> : be_kernel<10, MODE_STEP, FIX_NS, FIX_ND, false>;
+    L.epb = BLOCK_THREADS; W = -1;
+  } else if (fixed && W == 5) {
+    L.fn = pool ? be_kernel<5, MODE_STEP, FIX_NS, FIX_ND, true> : be_kernel<5, MODE_STEP, FIX_NS, FIX_ND, false>;
+    L.epb = BLOCK_THREADS; W = -1;
+  }
   switch (W) {
     case -1: break;
 #define BE_CASE(n) case n: L.fn = kernel_for<n>(mode); L.epb = envs_per_block(n); break;
@@ -3453,8 +3506,8 @@ Launch pick_kernel(const be_config& c, int mode, bool fixed_ok = false, int lane
     default: L.fn = kernel_for<0>(mode); L.epb = envs_per_block(0); staged = false; break;
   }
   if (L.fn) {
-    if (W == -1) snprintf(L.name, sizeof L.name, "be_kernel<%d, %d, %d, %d>", c.window, mode, FIX_NS, FIX_ND);
-    else snprintf(L.name, sizeof L.name, "be_kernel<%d, %d, 0, 0>", staged ? W : 0, mode);
+    if (W == -1) snprintf(L.name, sizeof L.name, "be_kernel<%d, %d, %d, %d, %s>", c.window, mode, FIX_NS, FIX_ND, pool ? "true" : "false");
+    else snprintf(L.name, sizeof L.name, "be_kernel<%d, %d, 0, 0, false>", staged ? W : 0, mode);
   }
   const int near_bytes = (nobs + 1) * BLOCK_THREADS * 4;   // +1: predicated pushes write one slot ahead
   const int stage_bytes = staged ? L.epb * F : 0;
@@ -3843,11 +3896,16 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   // be_step's two possible kernels, picked once (pick_kernel formats a name: not per launch)
   ctx->step_launch[0] = pick_kernel(ctx->cfg, MODE_STEP, false, ctx->step_lanes, ctx->step5_lpe);
   ctx->step_launch[1] = pick_kernel(ctx->cfg, MODE_STEP, true, ctx->step_lanes, ctx->step5_lpe);
-  {  // the autoreset pool, for the fixed-shape kernels that consume it (step2_kernel, stepw_kernel)
+  {  // the autoreset pool, for the fixed-shape kernels that consume it (step2_kernel, stepw_kernel, the one-lane kernel)
     const KFn f = ctx->step_launch[1].fn;
     const bool consumes = ctx->unit_moves && ctx->distinct_goals && !ctx->generic_only && cfg->autoreset &&
                           (f == step2_kernel<10, FIX_NS, FIX_ND, false> || f == stepw_kernel<5, FIX_NS, FIX_ND, 8, false> ||
-                           f == stepw_kernel<5, FIX_NS, FIX_ND, 4, false>);
+                           f == stepw_kernel<5, FIX_NS, FIX_ND, 4, false> ||
+                           // the one-lane kernel up to two waves per SIMD: 7.51-7.59 against 7.76-7.85 us at
+                           // 131 072 envs; at 262 144 (four waves per SIMD hide the reset draws, and the
+                           // fill costs more) 14.11-14.24 against 13.71-13.72 (profiles/r06_onelane_pool_ab.txt)
+                           ((f == be_kernel<10, MODE_STEP, FIX_NS, FIX_ND> || f == be_kernel<5, MODE_STEP, FIX_NS, FIX_ND>) &&
+                            (int64_t)cfg->num_envs <= (int64_t)2 * 64 * 4 * cus));
     bool want = consumes && (int64_t)cfg->num_envs <= POOL_MAX_ENVS;
     if (const char* v = getenv("BALLENV_POOL")) want = want && strcmp(v, "0") != 0;   // A/B: "0" = no pool
     ctx->pool_period = 128;

@@ -62,7 +62,7 @@ def test_multi_rank_engine_matches_one_rank(gpu, tmp_path, E, T, world):
     env.status()
     st = {k: v.cpu().numpy() for k, v in env.state_dict().items()}
     slots = env.stats_buf.cpu().numpy()
-    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5, true>" if E <= 98304 else "be_kernel<10, 0, 13, 5>")
+    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5, true>" if E <= 98304 else "be_kernel<10, 0, 13, 5, false>")   # (262 144: past the one-lane pool bound)
 
     assert done.sum() > E * T // 2000, "episodes must finish and autoreset during the run"
     for i, rk in enumerate(ranks):

@@ -35,7 +35,8 @@ def fixed_step_kernel(W, N=0):
         return "step2_kernel<10, 13, 5, true>"
     if W == 5 and N <= 64 * cus:
         return "stepw_kernel<5, 13, 5, 8, true>"
-    return f"be_kernel<{W}, 0, 13, 5>"
+    # the one-lane kernel takes the autoreset pool up to two waves per SIMD (128 x 4 x CUs envs)
+    return f"be_kernel<{W}, 0, 13, 5, {'true' if N <= 2 * 64 * 4 * cus else 'false'}>"
 
 
 def _random_lens(N, rng, limit=1000):
@@ -134,7 +135,7 @@ def test_step_kernel_top_of_id_space(gpu, W):
     off, k = (1 << 32) - N, SLICE
     a = N - k
     env = make_env(cfg_py, N, W, gpu, seed=0xBA11, env_offset=off, terminal_obs=True)
-    assert env.kernel_name("step") == fixed_step_kernel(W, N) == f"be_kernel<{W}, 0, 13, 5>"
+    assert env.kernel_name("step") == fixed_step_kernel(W, N) == f"be_kernel<{W}, 0, 13, 5, false>"
     cfg = cfg_py.to_abi(k, W, env_offset=off + a, seed=0xBA11)
     st = oracle.new_state(cfg)
     out = oracle.new_out(cfg, terminal=True)
@@ -336,7 +337,7 @@ def test_step_kernel_dispatch_by_batch(gpu, monkeypatch):
     monkeypatch.delenv("BALLENV_STEP_LPE", raising=False)
     cus = torch.cuda.get_device_properties(gpu).multi_processor_count
     cut = 96 * 4 * cus
-    for N, name in ((cut, "step2_kernel<10, 13, 5, true>"), (cut + 64, "be_kernel<10, 0, 13, 5>")):
+    for N, name in ((cut, "step2_kernel<10, 13, 5, true>"), (cut + 64, "be_kernel<10, 0, 13, 5, true>")):
         e = make_env(EnvConfig(), N, 10, gpu, seed=1)
         assert e.kernel_name("step") == name, (N, cus)
         e.close()
@@ -363,7 +364,7 @@ def test_step2_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
         envs.append(make_env(cfg_py, N, W, gpu, seed=31, terminal_obs=True, obs_f32=f32))
     monkeypatch.delenv("BALLENV_STEP_LPE")
     assert envs[0].kernel_name("step") == "step2_kernel<10, 13, 5, true>"
-    assert envs[1].kernel_name("step") == "be_kernel<10, 0, 13, 5>"
+    assert envs[1].kernel_name("step") == "be_kernel<10, 0, 13, 5, true>"
     lens = torch.from_numpy(_random_lens(N, np.random.default_rng(N), tl)).to(gpu)
     for e in envs:
         e.reset()
@@ -408,7 +409,7 @@ def test_step2_span_table_radius_bound(gpu, r_obs):
     N, a, k, W = 8192, 4096, SLICE, 10
     rng = np.random.default_rng(r_obs)
     env, cfg, st, out = _setup(cfg_py, N, W, gpu, a, k, seed=0x5A, rng=rng)
-    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5, true>" if r_obs + 5 <= 27 else "be_kernel<10, 0, 13, 5>")
+    assert env.kernel_name("step") == ("step2_kernel<10, 13, 5, true>" if r_obs + 5 <= 27 else "be_kernel<10, 0, 13, 5, true>")
     acts = env.sample_actions(60, seed=0x5A)
     lit = 0
     for t in range(60):
@@ -467,7 +468,7 @@ def test_stepw_equals_one_lane_kernel(gpu, N, tl, f32, monkeypatch):
         monkeypatch.setenv("BALLENV_STEP5_LPE", lpe)
         envs.append(make_env(cfg_py, N, W, gpu, seed=77, terminal_obs=True, obs_f32=f32))
     monkeypatch.delenv("BALLENV_STEP5_LPE")
-    assert [e.kernel_name("step") for e in envs] == ["be_kernel<5, 0, 13, 5>", "stepw_kernel<5, 13, 5, 8, true>",
+    assert [e.kernel_name("step") for e in envs] == ["be_kernel<5, 0, 13, 5, true>", "stepw_kernel<5, 13, 5, 8, true>",
                                                      "stepw_kernel<5, 13, 5, 4, true>"]
     lens = torch.from_numpy(_random_lens(N, np.random.default_rng(N + tl), tl)).to(gpu)
     for e in envs:
@@ -577,6 +578,6 @@ def test_fixed_kernels_batch_size_bound(gpu):
             names[n] = (lib.be_kernel_name(ctx, 0).decode(), lib.be_kernel_name(ctx, 2))   # rollout: NULL = loop
         finally:
             lib.be_destroy(ctx)
-    assert names[(1 << 29) - 1][0] == "be_kernel<10, 0, 13, 5>", names
-    assert names[1 << 29][0] == "be_kernel<10, 0, 0, 0>", names
+    assert names[(1 << 29) - 1][0] == "be_kernel<10, 0, 13, 5, false>", names   # (past 2^22 envs: no pool)
+    assert names[1 << 29][0] == "be_kernel<10, 0, 0, 0, false>", names
     assert names[1 << 29][1] is None or b"13, 5" not in names[1 << 29][1], names

@@ -35,7 +35,7 @@ def test_generic_kernel_obstacle_counts_vs_oracle(gpu, ns, nd, W, N, given):
                        goal_change_step=4, autoreset=True)
     cfg = cfg_py.to_abi(N, W, seed=31)
     env = make_env(cfg_py, N, W, gpu, seed=31, terminal_obs=True)
-    assert env.kernel_name("step").endswith(", 0, 0>"), env.kernel_name("step")   # the generic kernel
+    assert env.kernel_name("step").endswith(", 0, 0, false>"), env.kernel_name("step")   # the generic kernel
     st = oracle.new_state(cfg)
     out = oracle.new_out(cfg, terminal=True)
     oracle.reset(cfg, st, out)

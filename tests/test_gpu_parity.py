@@ -315,7 +315,7 @@ def test_goal_threshold_boundaries(gpu, W):
                 np.nextafter(s1800, 99.0), 7.5, 0.0, -1.0, 1e9):
         cfg_py = EnvConfig(autoreset=False, time_limit=0, threshold_goal=float(thr))
         env = make_env(cfg_py, N, W, gpu)   # (no autoreset: no pool, the plain fixed-shape variants)
-        assert env.kernel_name("step") in ("step2_kernel<10, 13, 5, false>", "stepw_kernel<5, 13, 5, 8, false>", f"be_kernel<{W}, 0, 13, 5>")
+        assert env.kernel_name("step") in ("step2_kernel<10, 13, 5, false>", "stepw_kernel<5, 13, 5, 8, false>", f"be_kernel<{W}, 0, 13, 5, false>")
         st = np_state(env)
         st["goal"][:] = (250, 250)
         st["agent"] = np.stack([250 + dx, 250 + dy], 1).astype(np.int16)
@@ -340,7 +340,7 @@ def test_reset_rejection_limit(gpu, W):
     cfg_py = EnvConfig(screen_width=20, screen_height=30, strip_obs_y=5, strip_goal_x=20, strip_agent_x=20,
                        time_limit=3)
     env = make_env(cfg_py, N, W, gpu, seed=seed)
-    assert env.kernel_name("step") in ("step2_kernel<10, 13, 5, true>", "stepw_kernel<5, 13, 5, 8, true>", f"be_kernel<{W}, 0, 13, 5>")
+    assert env.kernel_name("step") in ("step2_kernel<10, 13, 5, true>", "stepw_kernel<5, 13, 5, 8, true>", f"be_kernel<{W}, 0, 13, 5, true>")
     cfg = cfg_py.to_abi(N, W, seed=seed)
     st, out = oracle.new_state(cfg), oracle.new_out(cfg)
     env.reset()

@@ -3,8 +3,9 @@
 In Philox mode a reset into episode x is a pure function of (seed, global env id, x)
 (gym_ballenv/envs/ballenv_env.py:113-167 with the counter layout of oracle/ballenv_oracle.c:186-228),
 so pool_fill_kernel draws every env's resets into episodes e+1 and e+2 ahead of time and the
-fixed-shape step kernels (step2_kernel at W=10, stepw_kernel at W=5) copy the entry when the env
-finishes, drawing the reset inline only when the entry is stale.  These tests hold:
+fixed-shape step kernels (step2_kernel at W=10, stepw_kernel at W=5, and the one-lane kernel of the
+large batches at either W, forced here at small N by BALLENV_STEP_LPE / BALLENV_STEP5_LPE = 1) copy
+the entry when the env finishes, drawing the reset inline only when the entry is stale.  These tests hold:
   * the entries themselves against the oracle's reset of the same env into the same episode;
   * stepping with the pool against stepping without it (BALLENV_POOL=0), every output and the
     state, bit for bit, through refills, stale entries, masked resets and load_state;
@@ -25,7 +26,16 @@ from test_gpu_parity import KEYS, assert_state_equal, make_env, np_state
 
 pytestmark = pytest.mark.gpu
 
-KERNEL = {10: "step2_kernel<10, 13, 5, true>", 5: "stepw_kernel<5, 13, 5, 8, true>"}
+KERNEL = {10: "step2_kernel<10, 13, 5, true>", 5: "stepw_kernel<5, 13, 5, 8, true>",
+          (10, 1): "be_kernel<10, 0, 13, 5, true>", (5, 1): "be_kernel<5, 0, 13, 5, true>"}
+
+
+def _one_lane(monkeypatch, W, one):
+    """one=True: the one-lane fixed-shape kernel at this W (read at be_create); returns KERNEL's key"""
+    if one:
+        monkeypatch.setenv("BALLENV_STEP_LPE" if W == 10 else "BALLENV_STEP5_LPE", "1")
+        return (W, 1)
+    return W
 
 
 def _no_pool_env(cfg_py, N, W, dev, **kw):
@@ -87,11 +97,12 @@ def test_pool_entries_equal_the_oracle_reset(gpu, W):
     env.close()
 
 
-def _pair(cfg_py, N, W, dev, seed, **kw):
+def _pair(cfg_py, N, W, dev, seed, key=None, **kw):
+    key = W if key is None else key
     a = make_env(cfg_py, N, W, dev, seed=seed, **kw)
     b = _no_pool_env(cfg_py, N, W, dev, seed=seed, **kw)
     assert a.pool_bytes() > 0 and b.pool_bytes() == 0
-    assert a.kernel_name("step") == KERNEL[W] and b.kernel_name("step") == KERNEL[W].replace("true>", "false>")
+    assert a.kernel_name("step") == KERNEL[key] and b.kernel_name("step") == KERNEL[key].replace("true>", "false>")
     return a, b
 
 
@@ -110,14 +121,16 @@ def _same_step(a, b, act, t):
     return int(ra[2].sum())
 
 
-@pytest.mark.parametrize("W,N,period", [(10, 65536, 16), (10, 32768, 4), (5, 4096, 16), (5, 4096, 1)])
-def test_pool_steps_equal_inline_resets(gpu, W, N, period):
+@pytest.mark.parametrize("W,N,period,one", [(10, 65536, 16, False), (10, 32768, 4, False), (5, 4096, 16, False),
+                                            (5, 4096, 1, False), (10, 20000, 16, True), (5, 8192, 4, True)])
+def test_pool_steps_equal_inline_resets(gpu, W, N, period, one, monkeypatch):
     """The pool's env against an env without it, same ids and seed: 240 steps at TimeLimit 40 from
     random ep_len phases (thousands of resets, refills every `period` steps, entries going stale in
-    between), every output, the terminal obs and the state bit for bit; the stats slots equal."""
+    between), every output, the terminal obs and the state bit for bit; the stats slots equal.
+    one=True: the one-lane kernel (N = 20000: a partial last block)."""
     from gym_ballenv_amd.config import EnvConfig
     cfg_py = EnvConfig(time_limit=40)
-    a, b = _pair(cfg_py, N, W, gpu, seed=7, terminal_obs=True)
+    a, b = _pair(cfg_py, N, W, gpu, seed=7, key=_one_lane(monkeypatch, W, one), terminal_obs=True)
     a.pool_set_period(period)
     a.reset()
     b.reset()
@@ -134,14 +147,16 @@ def test_pool_steps_equal_inline_resets(gpu, W, N, period):
     b.close()
 
 
-@pytest.mark.parametrize("W", [10, 5])
-def test_pool_hit_copies_the_entry_and_stale_draws_inline(gpu, W):
+@pytest.mark.parametrize("W,one", [(10, False), (5, False), (10, True), (5, True)])
+def test_pool_hit_copies_the_entry_and_stale_draws_inline(gpu, W, one, monkeypatch):
     """A hit copies the entry: a poisoned entry (valid tag, a moved agent) is what the env resets to.
     A stale entry (tag of another episode) is not used: the env resets to the oracle's state."""
     from gym_ballenv_amd.config import EnvConfig
     N, seed, j = 256, 9, 77
     cfg_py = EnvConfig(time_limit=1000)
+    key = _one_lane(monkeypatch, W, one)
     env = make_env(cfg_py, N, W, gpu, seed=seed)
+    assert env.kernel_name("step") == KERNEL[key]
     env.pool_set_period(0)
     env.reset()
     e = int(env.episode[j].item())
@@ -173,8 +188,8 @@ def test_pool_hit_copies_the_entry_and_stale_draws_inline(gpu, W):
     env.close()
 
 
-@pytest.mark.parametrize("W,N", [(10, 4096), (5, 2048)])
-def test_pool_many_resets_per_wave_vs_oracle(gpu, W, N):
+@pytest.mark.parametrize("W,N,one", [(10, 4096, False), (5, 2048, False), (10, 3000, True), (5, 2048, True)])
+def test_pool_many_resets_per_wave_vs_oracle(gpu, W, N, one, monkeypatch):
     """TimeLimit 1: every env of every wave resets on every step.  No refills between steps, so step
     0 hits every entry (e+1), step 1 every e+2 entry; before step 2 a random half of the envs gets a
     fresh fill (others stay stale) and before step 3 a random third of the e+3 entries is invalidated
@@ -183,8 +198,9 @@ def test_pool_many_resets_per_wave_vs_oracle(gpu, W, N):
     from gym_ballenv_amd.config import EnvConfig
     seed = 31
     cfg_py = EnvConfig(time_limit=1)
+    key = _one_lane(monkeypatch, W, one)
     env = make_env(cfg_py, N, W, gpu, seed=seed)
-    assert env.kernel_name("step") == KERNEL[W]
+    assert env.kernel_name("step") == KERNEL[key]
     env.pool_set_period(0)
     cfg = cfg_py.to_abi(N, W, seed=seed)
     st, out = oracle.new_state(cfg), oracle.new_out(cfg)
@@ -218,15 +234,15 @@ def test_pool_many_resets_per_wave_vs_oracle(gpu, W, N):
     env.close()
 
 
-@pytest.mark.parametrize("W", [10, 5])
-def test_pool_masked_reset_and_load_state(gpu, W):
+@pytest.mark.parametrize("W,one", [(10, False), (5, False), (10, True)])
+def test_pool_masked_reset_and_load_state(gpu, W, one, monkeypatch):
     """Masked reset() and load_state() with the pool: both fill it for the state they leave (the
     entries need no invalidation -- each is a pure function of the env's id and episode), and the
     env then steps exactly as one without a pool; a reloaded blob replays its steps bit for bit."""
     from gym_ballenv_amd.config import EnvConfig
     N = 4096
     cfg_py = EnvConfig(time_limit=25)
-    a, b = _pair(cfg_py, N, W, gpu, seed=13)
+    a, b = _pair(cfg_py, N, W, gpu, seed=13, key=_one_lane(monkeypatch, W, one))
     a.reset()
     b.reset()
     acts = a.sample_actions(90, seed=14)

@@ -248,7 +248,7 @@ def test_w5_small_batch_kernels_non_default_radius(gpu, r_obs, monkeypatch):
     monkeypatch.setenv("BALLENV_STEP5_LPE", "1")
     monkeypatch.setenv("BALLENV_ROLLOUT5_LPE", "8")
     e = make_env(cfg, 4096, 5, gpu, seed=3)
-    assert e.kernel_name("rollout") == "rolloutw_kernel<5, 13, 5, 8>" and e.kernel_name("step") == "be_kernel<5, 0, 13, 5>"
+    assert e.kernel_name("rollout") == "rolloutw_kernel<5, 13, 5, 8>" and e.kernel_name("step") == "be_kernel<5, 0, 13, 5, true>"
     e.close()
     _run_pair(cfg, 4096, 5, 40, (15, 25), terminal=True)            # rolloutw vs one-lane steps
     monkeypatch.setenv("BALLENV_STEP5_LPE", "8")
@@ -323,7 +323,7 @@ def test_rolloutw_matches_steps(gpu, N, tl, lpe, terminal, monkeypatch):
     monkeypatch.setenv("BALLENV_STEP5_LPE", "1")
     e = make_env(EnvConfig(time_limit=tl), N, 5, gpu, seed=3)
     assert e.kernel_name("rollout") == f"rolloutw_kernel<5, 13, 5, {lpe}>"
-    assert e.kernel_name("step") == "be_kernel<5, 0, 13, 5>"
+    assert e.kernel_name("step") == "be_kernel<5, 0, 13, 5, true>"
     e.close()
     cfg = EnvConfig(time_limit=tl)
     lens = torch.from_numpy(np.random.default_rng(N + tl).integers(0, tl, N).astype(np.int32)).to(gpu)

@@ -29,6 +29,7 @@ if bp:
     print('%-8s r$r: board step %.3f  fused %.3f us' % ('$v', bp['kernel_us_mean'], bp['fused']['kernel_us_per_step']), flush=True)
     raise SystemExit
 s = '%-8s r$r: step %.3f  config2 %.3f  config4@%d %.3f us' % ('$v', d['roofline']['kernel_us_mean'], d['config2']['kernel_us_mean'], d['config4']['envs_per_rank'], d['config4']['kernel_us_mean'])
+if d.get('large_batch'): s += '  large %.3f' % d['large_batch']['kernel_us_mean']
 if d.get('fused_rollout'): s += '  fused %.3f' % d['fused_rollout']['kernel_us_per_step']
 if d.get('policy_rollout'): s += '  policy %.3f' % d['policy_rollout']['kernel_us_per_step']
 print(s, flush=True)"

@@ -11,7 +11,7 @@ COMMON="--no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 --t
 for n in ${SIZES:-262144 131072 65536 32768}; do
   PASSES="FETCH_SIZE WRITE_SIZE" timeout -k 10 400 bash tools/pmc_passes.sh pmc_c4/g$n $COMMON --config4-envs $n || exit 1
   # grid = the kernel's threads at this size (step2: 2 lanes per env, 128-env blocks; one lane: 256-env blocks)
-  k="be_kernel<10, 0, 13, 5>"; g=$(( (n + 255) / 256 * 256 ))
-  [ $n -le 98304 ] && { k="step2_kernel<10, 13, 5>"; g=$(( (n + 127) / 128 * 256 )); }
+  k="be_kernel<10, 0, 13, 5, $([ $n -le 131072 ] && echo true || echo false)>"; g=$(( (n + 255) / 256 * 256 ))
+  [ $n -le 98304 ] && { k="step2_kernel<10, 13, 5, true>"; g=$(( (n + 127) / 128 * 256 )); }
   python3 tools/pmc_report.py gpurun_out/pmc_c4/g$n "$k" $n --grid $g --out gpurun_out/pmc_c4/${R}_pmc_config4_$n.json | tail -2
 done

@@ -38,7 +38,7 @@ if [ "${PMC:-1}" = "1" ]; then
   step pmc_c2_large 600 bash tools/pmc_passes.sh ${ROUND:-r04}_check/pmc --no-cpu-baseline --steps 10 --warmup 2 --settle 10 --policy-steps 0 \
       --board-steps 0 --rollout-steps 0 --cold-steps 0 --from-reset-steps 0 --blocks-launches 0 --config2-steps 200 --large-steps 100
   python tools/pmc_report.py $O/pmc "stepw_kernel<5, 13, 5, 8>" 4096 --out $O/${ROUND:-r04}_pmc_config2.json > /dev/null
-  python tools/pmc_report.py $O/pmc "be_kernel<10, 0, 13, 5>" 1048576 --out $O/${ROUND:-r04}_pmc_large_batch.json > /dev/null
+  python tools/pmc_report.py $O/pmc "be_kernel<10, 0, 13, 5, true>" 1048576 --out $O/${ROUND:-r04}_pmc_large_batch.json > /dev/null
   step pmc_step 700 bash tools/pmc_bench.sh
   tail -1 $O/pmc_step.log
 fi

@@ -64,8 +64,8 @@ if head:
         per = (sum(e - s for s, e in reg) + sum(e - s for s, e in fl)) / len(reg) / 1e3
         print(f"  + {len(fl)} pool_fill_kernel launches in that region, {avg_us(fl):.3f} us each: "
               f"{per:.3f} us of kernel time per step, the fills included")
-for prefix, n, grid, what in (("be_kernel<10, 0, 13, 5>", 262144, 262144, "config 4 at one rank"),
-                              ("be_kernel<10, 0, 13, 5>", 131072, 131072, "config 4's 2-GPU shard"),
+for prefix, n, grid, what in (("be_kernel<10, 0, 13, 5, true>", 262144, 262144, "config 4 at one rank"),
+                              ("be_kernel<10, 0, 13, 5, true>", 131072, 131072, "config 4's 2-GPU shard"),
                               ("step2_kernel<10, 13, 5, true>", 32768, 65536, "config 4's 8-GPU shard")):
     k = find(prefix)
     L = by_grid.get((k, grid), [])
@@ -74,7 +74,7 @@ for prefix, n, grid, what in (("be_kernel<10, 0, 13, 5>", 262144, 262144, "confi
         print(f"{k} ({what}, {n} envs): the last 1000 launches at that size average {avg_us(reg):.3f} us; "
               f"{n} x 390 B / that = {n * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
 for prefix, last, what in (("stepw_kernel<5, 13, 5, 8, true>", 1000, "config 2, 4096 envs, W=5"),
-                           ("be_kernel<10, 0, 13, 5>", 200, "2^20 envs, large_batch"),
+                           ("be_kernel<10, 0, 13, 5, true>", 200, "2^20 envs, large_batch"),
                            ("board_kernel<6, false, 1", 1000, "createBoard step, 65536 envs"),
                            ("board_kernel<6, true, 1", 10, "createBoard fused, 100 steps per launch"),
                            ("rollout_kernel<10, 13, 5, 13, 2, 10>", 10, "config 5 fused, 100 steps per launch"),
