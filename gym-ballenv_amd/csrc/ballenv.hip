@@ -1462,7 +1462,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
     if ((tid & 63) == 0) atomicOr(p.status, (int)f);
   }
   WaveStats ws{0.0, 0.0, 0.0, 0.0, INFINITY, -INFINITY}, ws_hi = ws;
-  if (MODE == MODE_STEP && p.stats && !DBG(DBG_NO_STATS)) {   // all lanes converged here
+  // (POOL: after the resets, below -- a reset leaves fin_ret / fin_len alone -- so that the two halves'
+  // sums are not live across the pool's loads: 148 -> 107 VGPRs, four waves per SIMD again)
+  if (!POOL && MODE == MODE_STEP && p.stats && !DBG(DBG_NO_STATS)) {   // all lanes converged here
     if constexpr (FIXED) {   // one slot per 32 envs (be_stats_slots): the wave's two halves
       wave_stats2(done && lead, fin_ret, fin_len, ws, ws_hi);
     } else {
@@ -1603,6 +1605,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void be_kernel(KParams p) {
       wave_resets<WT, NSC, NDC, 64>(p, t, m, i, gid, episode, ax, ay, gx, gy, nl.cnt, xrows, &s_rows[(tid >> 6) * 16][0],
                                     osink, esink);
   }
+  if (POOL && p.stats && !DBG(DBG_NO_STATS)) wave_stats2(done && lead, fin_ret, fin_len, ws, ws_hi);   // (converged)
   DIAG(3);
 
   // ---- observation (prep_state4)
@@ -3898,6 +3901,8 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
   ctx->step_launch[1] = pick_kernel(ctx->cfg, MODE_STEP, true, ctx->step_lanes, ctx->step5_lpe);
   {  // the autoreset pool, for the fixed-shape kernels that consume it (step2_kernel, stepw_kernel, the one-lane kernel)
     const KFn f = ctx->step_launch[1].fn;
+    int64_t onelane_max = (int64_t)2 * 64 * 4 * cus;   // BALLENV_POOL_ONELANE_MAX: the bound below, for A/B runs
+    if (const char* v = getenv("BALLENV_POOL_ONELANE_MAX")) onelane_max = atoll(v);
     const bool consumes = ctx->unit_moves && ctx->distinct_goals && !ctx->generic_only && cfg->autoreset &&
                           (f == step2_kernel<10, FIX_NS, FIX_ND, false> || f == stepw_kernel<5, FIX_NS, FIX_ND, 8, false> ||
                            f == stepw_kernel<5, FIX_NS, FIX_ND, 4, false> ||
@@ -3905,7 +3910,7 @@ int be_create(const be_config* cfg, int32_t device, be_ctx** out) {
                            // 131 072 envs; at 262 144 (four waves per SIMD hide the reset draws, and the
                            // fill costs more) 14.11-14.24 against 13.71-13.72 (profiles/r06_onelane_pool_ab.txt)
                            ((f == be_kernel<10, MODE_STEP, FIX_NS, FIX_ND> || f == be_kernel<5, MODE_STEP, FIX_NS, FIX_ND>) &&
-                            (int64_t)cfg->num_envs <= (int64_t)2 * 64 * 4 * cus));
+                            (int64_t)cfg->num_envs <= onelane_max));
     bool want = consumes && (int64_t)cfg->num_envs <= POOL_MAX_ENVS;
     if (const char* v = getenv("BALLENV_POOL")) want = want && strcmp(v, "0") != 0;   // A/B: "0" = no pool
     ctx->pool_period = 128;
