@@ -1,15 +1,15 @@
 """Per-region kernel averages from a rocprofv3 kernel trace (run_kernel_trace.csv) of the default
-`python3 bench.py` command: the headline's timed region, config 2's and the 2^20-env leg's.
+`python3 bench.py` command: the headline's timed region, config 2's, config 4's and the 2^20-env leg's.
 
     python tools/trace_regions.py <kernel_trace.csv> [--warmup 100] [--untimed 1000] [--steps 1000]
 
 bench.py's headline leg launches the step kernel `warmup` times eagerly, replays the captured graph
 for `untimed` steps (settle), then times `steps` launches: launches warmup+untimed+1 ..
-warmup+untimed+steps of the headline kernel are the timed region.  The config-2 and large-batch legs
-are the last 1000 / 200 launches of their kernels; config 4 at one rank (262 144 envs, the one-lane
-kernel) and its per-rank shards (131 072 envs one-lane, 32 768 envs step2_kernel) are the last 1000
-launches of that kernel at that grid size (threads: Grid_Size; the one-lane kernel runs 1 thread per env,
-step2_kernel 2)."""
+warmup+untimed+steps of the headline kernel are the timed region.  The config-2 leg is the last 1000
+launches of its kernel; config 4 at one rank (262 144 envs, the one-lane kernel without the pool), its
+per-rank shards (131 072 envs one-lane with the pool, 32 768 envs step2_kernel) and the 2^20-env leg
+are the last 1000 (200) launches of that kernel at that grid size (threads: Grid_Size; the one-lane
+kernel runs 1 thread per env, step2_kernel 2)."""
 import argparse
 import csv
 import statistics
@@ -64,18 +64,18 @@ if head:
         per = (sum(e - s for s, e in reg) + sum(e - s for s, e in fl)) / len(reg) / 1e3
         print(f"  + {len(fl)} pool_fill_kernel launches in that region, {avg_us(fl):.3f} us each: "
               f"{per:.3f} us of kernel time per step, the fills included")
-for prefix, n, grid, what in (("be_kernel<10, 0, 13, 5, true>", 262144, 262144, "config 4 at one rank"),
-                              ("be_kernel<10, 0, 13, 5, true>", 131072, 131072, "config 4's 2-GPU shard"),
-                              ("step2_kernel<10, 13, 5, true>", 32768, 65536, "config 4's 8-GPU shard")):
+for prefix, n, grid, last, what in (("be_kernel<10, 0, 13, 5, false>", 262144, 262144, 1000, "config 4 at one rank"),
+                                    ("be_kernel<10, 0, 13, 5, true>", 131072, 131072, 1000, "config 4's 2-GPU shard"),
+                                    ("step2_kernel<10, 13, 5, true>", 32768, 65536, 1000, "config 4's 8-GPU shard"),
+                                    ("be_kernel<10, 0, 13, 5, false>", 1 << 20, 1 << 20, 200, "2^20 envs, large_batch")):
     k = find(prefix)
     L = by_grid.get((k, grid), [])
-    if len(L) >= 1000:
-        reg = L[-1000:]
-        print(f"{k} ({what}, {n} envs): the last 1000 launches at that size average {avg_us(reg):.3f} us; "
+    if len(L) >= last:
+        reg = L[-last:]
+        print(f"{k} ({what}, {n} envs): the last {last} launches at that size average {avg_us(reg):.3f} us; "
               f"{n} x 390 B / that = {n * 390 / (avg_us(reg) * 1e-6) / 1e12:.2f} TB/s")
 for prefix, last, what in (("stepw_kernel<5, 13, 5, 8, true>", 1000, "config 2, 4096 envs, W=5"),
-                           ("be_kernel<10, 0, 13, 5, true>", 200, "2^20 envs, large_batch"),
-                           ("board_kernel<6, false, 1", 1000, "createBoard step, 65536 envs"),
+                           ("board_kernel<6, false, 1, true>", 1000, "createBoard step, 65536 envs"),
                            ("board_kernel<6, true, 1", 10, "createBoard fused, 100 steps per launch"),
                            ("rollout_kernel<10, 13, 5, 13, 2, 10>", 10, "config 5 fused, 100 steps per launch"),
                            ("blocks_kernel", 200, "prep_state2 blocks (last leg size)")):
