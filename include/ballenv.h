@@ -243,8 +243,9 @@ int be_load_state(be_ctx* ctx, const be_state* st, const void* blob, void* strea
 /* ---- the autoreset pool (a cache inside the context; no reference counterpart) ----
  * In Philox mode BallEnv.reset (ballenv_env.py:113-167) of env i into episode e is a pure
  * function of (seed, global id, e) and the config.  When be_step's kernel is a fixed-shape one
- * that consumes it (step2_kernel at W=10, stepw_kernel at W=5, the reference's 13 + 5 obstacles),
- * the context holds, per env, the precomputed resets into episodes e+1 and e+2 (ep = the env's
+ * that consumes it (step2_kernel at W=10, stepw_kernel at W=5, and the one-lane kernel up to
+ * 128 x 4 x CUs envs -- two waves per SIMD; past that its waves hide the draws and the pool
+ * measured slower -- all at the reference's 13 + 5 obstacles), the context holds, per env, the precomputed resets into episodes e+1 and e+2 (ep = the env's
  * episode); a finishing env copies its entry instead of drawing the reset on the step's critical
  * path, and draws it inline as before when the entry is stale.  Results are bit-identical either
  * way -- the pool changes timing only.  be_reset and be_load_state fill it after their own work,
