@@ -135,3 +135,62 @@ def test_graph_captured_batched_step_api(gpu):
     for e in (eager, graphed):
         e.status()
         e.close()
+
+
+@pytest.mark.parametrize("W,N", [(10, 65536), (5, 4096)])
+def test_short_graph_with_captured_pool_fill(gpu, W, N):
+    """A graph of 8 steps plus a captured be_pool_fill, replayed 40 times (INTEGRATION.md's recipe for
+    short graphs): the same trajectory as an env without the pool stepping eagerly.  TimeLimit 12, so
+    every env resets several times and only the captured fills keep its entries current; the pool's
+    own entries afterwards are current for the env's next two episodes (the captured fill ran)."""
+    import os
+    from gym_ballenv_amd import _abi
+    from gym_ballenv_amd.config import EnvConfig
+    K, R = 8, 40
+    cfg_py = EnvConfig(time_limit=12)
+    graphed = make_env(cfg_py, N, W, gpu, seed=77)
+    os.environ["BALLENV_POOL"] = "0"
+    try:
+        eager = make_env(cfg_py, N, W, gpu, seed=77)
+    finally:
+        del os.environ["BALLENV_POOL"]
+    assert graphed.pool_bytes() > 0 and eager.pool_bytes() == 0
+    graphed.pool_set_period(0)          # no host-counted fills: only the captured one
+    acts = eager.sample_actions(K, seed=9)
+    for e in (eager, graphed):
+        e.reset()
+    lib, ctx, st, out = graphed._lib, graphed._ctx, C.byref(graphed._st), C.byref(graphed._out)
+    rec = {k: torch.empty((K,) + tuple(getattr(graphed, k).shape), dtype=getattr(graphed, k).dtype, device=gpu)
+           for k in ("obs", "reward", "done")}
+    side = torch.cuda.Stream(gpu)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        cs = C.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+        for t in range(K):
+            rc = lib.be_step(ctx, st, C.c_void_p(acts[t].data_ptr()), None, None, out, cs)
+            if rc:
+                _abi.check(rc, ctx)
+            for k, buf in rec.items():
+                buf[t].copy_(getattr(graphed, k))
+        _abi.check(lib.be_pool_fill(ctx, st, cs), ctx)
+    n_done = 0
+    for r in range(R):
+        g.replay()
+        for t in range(K):
+            obs, reward, done, _ = eager.step(acts[t])
+            n_done += int(done.sum())
+            for k, v in (("obs", obs), ("reward", reward), ("done", done)):
+                assert torch.equal(rec[k][t], v), f"{k} replay {r} t={t}"
+    torch.cuda.synchronize(gpu)
+    a, b = np_state(eager), np_state(graphed)
+    for k in KEYS:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert n_done > 4 * N, n_done
+    ep = graphed.episode.cpu().numpy().view(np.uint32)
+    for i in np.random.default_rng(W).choice(N, 16, replace=False):
+        for x in (int(ep[i]) + 1, int(ep[i]) + 2):
+            words, _ = graphed.pool_entry(int(i), x & 1)
+            assert words[0] == x and words[3] & (1 << 30), (i, x)
+    for e in (eager, graphed):
+        e.status()
+        e.close()
