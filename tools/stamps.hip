@@ -128,17 +128,25 @@ int main(int argc, char** argv) {
       std::vector<int> idx;
       for (int w = 0; w < DW; ++w) if (rt[w * DP + 0]) idx.push_back(w);
       std::sort(idx.begin(), idx.end(), [&](int a, int b) { return rt[a * DP + 6] > rt[b * DP + 6]; });
-      std::vector<double> end_r, end_n;
+      std::vector<double> end_r, end_n, end_p, hit_wait;
       std::vector<std::vector<double>> end_x(16);
+      // POOL_STAMP=1 (step2_kernel<..., true>): stamp 9 = a pool entry landed in this launch (a hit wave)
+      const bool pool_stamp = getenv("POOL_STAMP") && atoi(getenv("POOL_STAMP"));
       for (int w : idx) {
         const unsigned long long* r = &rt[w * DP];
         const bool rs = r[12] >= r[0] && r[12] <= r[6] && r[12];
-        (rs ? end_r : end_n).push_back((r[6] - t0) * 0.01);
+        const bool ps = pool_stamp && !rs && r[9] >= r[0] && r[9] <= r[6] && r[9];
+        (rs ? end_r : ps ? end_p : end_n).push_back((r[6] - t0) * 0.01);
+        if (ps) hit_wait.push_back((double)(cy[w * DP + 9] - cy[w * DP + 10]));
         end_x[(hw[w] >> 28) & 15].push_back((r[6] - t0) * 0.01);
       }
       printf("  tail: end us of reset waves (%zu) p50 %.2f max %.2f | other waves (%zu) p50 %.2f p90 %.2f p99 %.2f max %.2f\n",
              end_r.size(), end_r.empty() ? 0 : pct(end_r, .5), end_r.empty() ? 0 : pct(end_r, 1), end_n.size(), pct(end_n, .5),
              pct(end_n, .9), pct(end_n, .99), pct(end_n, 1));
+      if (pool_stamp)
+        printf("  tail: end us of pool-hit waves (%zu) p50 %.2f max %.2f; obstacle tests -> entry landed: cycles p50 %.0f max %.0f\n",
+               end_p.size(), end_p.empty() ? 0 : pct(end_p, .5), end_p.empty() ? 0 : pct(end_p, 1),
+               hit_wait.empty() ? 0 : pct(hit_wait, .5), hit_wait.empty() ? 0 : pct(hit_wait, 1));
       for (int x = 0; x < 16; ++x)
         if (!end_x[x].empty()) printf("  tail: xcc %d end p50 %.2f p90 %.2f max %.2f us\n", x, pct(end_x[x], .5), pct(end_x[x], .9), pct(end_x[x], 1));
       {   // -DBE_RESET_STAMPS builds: reset waves' phase A split (2 -> 7 -> 8 -> 9 -> 10 -> 12)
@@ -161,8 +169,10 @@ int main(int argc, char** argv) {
         const unsigned long long* r = &rt[w * DP];
         const unsigned long long* c = &cy[w * DP];
         const unsigned h = hw[w];
+        const bool rsw = r[12] >= r[0] && r[12] <= r[6] && r[12];
+        const bool psw = pool_stamp && !rsw && r[9] >= r[0] && r[9] <= r[6] && r[9];
         printf("    w%5d %.2f %.2f %s x%u/se%u/cu%2u |", w, (r[0] - t0) * 0.01, (r[6] - t0) * 0.01,
-               (r[12] >= r[0] && r[12] <= r[6] && r[12]) ? "R" : "-", (h >> 28) & 15, (h >> 13) & 3, (h >> 8) & 15);
+               rsw ? "R" : psw ? "P" : "-", (h >> 28) & 15, (h >> 13) & 3, (h >> 8) & 15);
         for (int p = 0; p < 6; ++p) printf(" %6llu", c[p + 1] - c[p]);
         printf("\n");
       }
