@@ -2034,7 +2034,9 @@ __global__ __launch_bounds__(S2_CT, 2) void step2_kernel(KParams p) {
     for (int j = 0; j < 7; ++j) qb[j] = pool_ld<uint4>(p.pool, bo, 16u * j);
     __builtin_amdgcn_s_waitcnt(0);   // here, in the branch: no pending pool load past its end
   }
-  if (__ballot(ptry)) DIAG(9);   // (stamps build: this wave's entries landed; nothing in production)
+#ifdef BE_DIAG_STAMPS
+  if (__ballot(ptry)) DIAG(9);   // (stamps build: this wave's entries landed)
+#endif
 #endif
   if (valid) {   // both lanes of the pair store the env's scalars (the same value to the same address:
                  // one full-wave store per array, no per-lane pointer selects or exec masking)
