@@ -1,6 +1,8 @@
-"""Host cost of BatchedBallEnv.step() per call: the current class against round 4's
-(tools/diag/batched_r04.py = `git show 3673bc0:gym-ballenv_amd/batched.py`), interleaved, the
-bench's eager_step method (65 536 envs, W=10, actions from acts.random_ each step, 1000 calls).
+"""Host cost of BatchedBallEnv.step() per call: the current class against an earlier one,
+interleaved, the bench's eager_step method (65 536 envs, W=10, actions from acts.random_ each step,
+1000 calls).  The baseline class file is argv[1] (default tools/diag/batched_r04.py = `git show
+3673bc0:gym-ballenv_amd/batched.py`; round 6: tools/eager_base/batched_head.py = the class before the
+raw-stream call), its label argv[2].
 """
 import importlib.util
 import os
@@ -13,7 +15,9 @@ import torch  # noqa: E402
 
 import gym_ballenv_amd as gb  # noqa: E402
 
-spec = importlib.util.spec_from_file_location("gym_ballenv_amd.batched_r04", os.path.join(ROOT, "tools/diag/batched_r04.py"))
+BASE = sys.argv[1] if len(sys.argv) > 1 else "tools/diag/batched_r04.py"
+LABEL = sys.argv[2] if len(sys.argv) > 2 else "r04"
+spec = importlib.util.spec_from_file_location("gym_ballenv_amd.batched_base", os.path.join(ROOT, BASE))
 old = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(old)
 
@@ -41,7 +45,7 @@ def run(cls, T=1000, N=65536):
     return call / T * 1e6, el / T * 1e6
 
 
-for rep in range(3):
-    for name, cls in (("r04", old.BatchedBallEnv), ("r05", gb.BatchedBallEnv)):
+for rep in range(int(os.environ.get("REPS", "3"))):
+    for name, cls in ((LABEL, old.BatchedBallEnv), ("new", gb.BatchedBallEnv)):
         c, it = run(cls)
         print(f"{name} rep {rep}: host us per step() call {c:.2f}, wall us per loop iteration {it:.2f}", flush=True)

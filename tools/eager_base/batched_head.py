@@ -116,13 +116,9 @@ class BatchedBallEnv:
         # torch without it falls back to the public Stream object (same handle, a little slower)
         raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
         if raw is not None:
-            self._stream_int = lambda: raw(dev)
+            self._stream = lambda: C.c_void_p(raw(dev))
         else:
-            self._stream_int = lambda: torch.cuda.current_stream(dev).cuda_stream
-        self._stream = lambda: C.c_void_p(self._stream_int())
-        # step()'s common call: the foreign function looked up once, and the stream handle passed
-        # as the plain int (ctypes' c_void_p argtype converts it; no wrapper object per call)
-        self._be_step = self._lib.be_step
+            self._stream = lambda: C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
     def _stream(self):
         """The caller's current stream on this env's device (raw handle; replaced per instance in
@@ -207,7 +203,7 @@ class BatchedBallEnv:
                 ptr = a.data_ptr()
             else:
                 ptr = self._a_ptr
-            rc = self._be_step(self._ctx, self._st_ref, ptr, None, None, self._out_ref, self._stream_int())
+            rc = self._lib.be_step(self._ctx, self._st_ref, ptr, None, None, self._out_ref, self._stream())
             if rc:
                 _abi.check(rc, self._ctx)
             return self._obs_ret, self.reward, self.done, self._info
