@@ -194,3 +194,51 @@ def test_short_graph_with_captured_pool_fill(gpu, W, N):
     for e in (eager, graphed):
         e.status()
         e.close()
+
+
+
+@pytest.mark.parametrize("W,N", [(10, 4096), (5, 4096)])
+def test_step_runs_on_the_callers_stream(gpu, W, N):
+    """step() launches on the caller's current stream (the raw handle torch reports), ordered
+    after the work the caller queued there: the actions are written on a side stream behind a
+    ~20-ms spin, and the step on that stream must see them.  A step launched on any other stream
+    would read the old actions at once and give another trajectory."""
+    from gym_ballenv_amd.config import EnvConfig
+    cfg_py = EnvConfig(time_limit=40)
+    env, ref = (make_env(cfg_py, N, W, gpu, seed=11) for _ in range(2))
+    env.reset()
+    ref.reset()
+    new = ref.sample_actions(3, seed=9)
+    exp = []
+    for t in range(3):
+        exp.append([x.clone() for x in ref.step(new[t], copy=True)[:3]])
+    acts = torch.full((N,), 5, dtype=torch.uint8, device=gpu)   # action 5 = (0, 0): another trajectory
+    torch.cuda.synchronize(gpu)
+    side = torch.cuda.Stream(gpu)
+    got = []
+    with torch.cuda.stream(side):
+        for t in range(3):
+            torch.cuda._sleep(50_000_000)
+            acts.copy_(new[t])
+            got.append([x.clone() for x in env.step(acts)[:3]])
+    side.synchronize()
+    for t in range(3):
+        for k, (a, b) in enumerate(zip(exp[t], got[t])):
+            assert torch.equal(a, b), (t, ("obs", "reward", "done")[k])
+    for k in KEYS:
+        assert torch.equal(getattr(env, k), getattr(ref, k)), k
+    # the check has teeth: the same calls with step() sent to the default stream instead read the
+    # actions before the side stream writes them
+    wrong = make_env(cfg_py, N, W, gpu, seed=11)
+    wrong.reset()
+    wrong._stream_int = lambda: torch.cuda.default_stream(gpu).cuda_stream
+    acts2 = torch.full((N,), 5, dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize(gpu)
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(50_000_000)
+        acts2.copy_(new[0])
+        wrong.step(acts2)
+    torch.cuda.synchronize(gpu)
+    assert not torch.equal(wrong.reward, exp[0][1])
+    for e in (env, ref, wrong):
+        e.close()
