@@ -24,7 +24,7 @@ from oracle import oracle  # noqa: E402
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 1400
 PERIODS = [int(p) for p in sys.argv[3:]] or [16, 32, 64, 128, 512]
-SKIP = 400          # bench.py's settle: the timed region starts past the post-reset transient
+SKIP = int(os.environ.get("SKIP", "400"))   # bench.py's settle: the timed region starts past the post-reset transient
 EPW = 32            # envs per wave of step2_kernel (W=10)
 
 cfg = EnvConfig().to_abi(N, 10, 0, 0xBA11)
